@@ -1,0 +1,87 @@
+// fks_internal.h -- shared declarations of libfks.so (host + device).
+#pragma once
+
+#include <cerrno>
+#include <cstddef>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "fks.h"
+
+namespace fks {
+
+// Exceptions never cross the C ABI: fks_capi.cpp converts them to codes.
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+// ---- MT19937 constants (MT19937RNGEngine.h:21-25) ----
+constexpr int kMtN = 624;
+constexpr int kMtM = 397;
+constexpr uint32_t kMatrixA = 0x9908b0dfu;
+
+// ---- jump-ahead (fks_gf2.cpp) ----
+int jump_poly_words();  // 312
+void jump_polys_for_blocks(const std::vector<int64_t>& blocks, std::vector<uint64_t>& out);
+void host_jump_window(uint64_t seed, int64_t block, uint32_t* out624);
+
+// ---- Box-Muller tables for the 8-bit (bf16) and 11-bit (f16) uniforms (fks_tables.cpp) ----
+// radius[a], cos[b], sin[b] as float values of the reduced type, exactly as
+// normal_fill_16<scalar_t> (DistributionTemplates.h:139-149) computes them.
+struct Tables {
+  float r_bf16[256], c_bf16[256], s_bf16[256];
+  float r_f16[2048], c_f16[2048], s_f16[2048];
+};
+const Tables& tables();
+
+// ---- device-side descriptors ----
+// A regular segment: a tensor (or the part of it) whose 16-element Box-Muller
+// blocks sit on 16-aligned stream positions, so each 16-block lies inside one
+// 624-word MT block.
+struct DevSeg {
+  int64_t start;   // stream position of element 0
+  int64_t numel;   // multiple of 16
+  uint64_t ptr;    // device address of element 0
+  float lr;
+  float wd;
+  uint32_t flags;  // FKS_HAS_WD
+  int32_t dtype;
+};
+static_assert(sizeof(DevSeg) == 40, "DevSeg layout");
+
+constexpr int kApplyThreads = 320;  // 312 Box-Muller pairs per 624-word block + 8 idle lanes
+constexpr int kMaxSeedsPerPass = 28;  // MT states resident in LDS per workgroup (28 x 2496 B)
+constexpr int kJumpThreads = 640;
+constexpr int kJumpXLen = 19937 + 624;  // x[0..20560]: y[i + w] = x[i + w + 1], i < 19937, w < 624
+
+enum ApplyMode : int { kModeUpdate = 0, kModePerturb = 1, kModeWriteZ = 2 };
+
+struct ApplyArgs {
+  const uint32_t* states;       // [nseeds][nchunks][624] generator windows at chunk starts
+  const float* g;               // [nseeds] update multiplier (mode 0); perturb scales ride in DevSeg::lr
+  const DevSeg* segs;           // regular segments of this launch's dtype, sorted by start
+  const int64_t* chunk_block;   // [nchunks + 1] first MT block of each chunk
+  int32_t nsegs;
+  int32_t nchunks;
+  int32_t nseeds;
+  int32_t mode;
+};
+
+struct JumpArgs {
+  const uint64_t* seeds;        // [nseeds]
+  const uint64_t* polys;        // [nchunks][312] t^(624*b-1) mod phi (unused for b == 0)
+  const int64_t* chunk_block;   // [nchunks + 1]
+  uint32_t* states;             // [nseeds][nchunks][624]
+  int32_t nchunks;
+  int32_t chunks_per_wg;
+};
+
+// launchers (fks_device.hip); return hipError_t as int
+int launch_jump(const JumpArgs& a, int nseeds, void* stream);
+int launch_apply(int dtype, const ApplyArgs& a, void* stream);
+int device_cu_count();
+
+}  // namespace fks

@@ -1,0 +1,81 @@
+"""ctypes binding of libfks.so (C ABI: include/fks.h).
+
+The library sits next to this file (built in-tree by fate-llm_amd/Makefile).  There
+is no CPU fallback: if the library or a HIP device is missing, every codec call
+raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfks.so")
+
+F32, BF16, F16 = 0, 1, 2
+HAS_WD, FROZEN = 1, 2
+VALUE_SCALAR, VALUE_TENSOR = 0, 1
+ABI_VERSION = 1
+
+# every symbol include/fks.h declares (checked by tests/test_capi_symbols.py)
+EXPORTED = (
+    "fks_workspace_size", "fks_directional_step", "fks_perturb", "fks_normal", "fks_last_error",
+    "fks_abi_version", "fks_build_target", "fks_host_jump_window", "fks_host_tables",
+)
+
+
+class FksTensor(ctypes.Structure):
+    """struct fks_tensor (include/fks.h)."""
+
+    _fields_ = [
+        ("data", ctypes.c_void_p),
+        ("numel", ctypes.c_int64),
+        ("dtype", ctypes.c_int32),
+        ("flags", ctypes.c_uint32),
+        ("lr", ctypes.c_float),
+        ("wd", ctypes.c_float),
+    ]
+
+
+class FksError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libfks error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load libfks.so (raises OSError if it has not been built)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"{LIB_PATH} not built; run `make -C fate-llm_amd` (hipcc, gfx950)")
+        L = ctypes.CDLL(LIB_PATH)
+        P, c_i32, c_u64, c_sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64, ctypes.c_size_t
+        L.fks_workspace_size.argtypes = [P, c_i32, c_i32, ctypes.POINTER(c_sz)]
+        L.fks_directional_step.argtypes = [P, c_i32, P, P, c_i32, c_i32, P, c_sz, P]
+        L.fks_perturb.argtypes = [P, c_i32, c_u64, P, P, c_sz, P]
+        L.fks_normal.argtypes = [P, c_i32, c_u64, P, c_sz, P]
+        L.fks_last_error.restype = ctypes.c_char_p
+        L.fks_abi_version.restype = c_i32
+        L.fks_build_target.restype = ctypes.c_char_p
+        L.fks_host_jump_window.argtypes = [c_u64, ctypes.c_int64, P]
+        L.fks_host_tables.argtypes = [c_i32, P, P, P, c_i32]
+        for name in ("fks_workspace_size", "fks_directional_step", "fks_perturb", "fks_normal",
+                     "fks_host_jump_window", "fks_host_tables"):
+            getattr(L, name).restype = ctypes.c_int
+        if L.fks_abi_version() != ABI_VERSION:
+            raise OSError(f"libfks.so ABI {L.fks_abi_version()} != {ABI_VERSION}")
+        _lib = L
+        return L
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise FksError(rc, load().fks_last_error().decode(errors="replace"))

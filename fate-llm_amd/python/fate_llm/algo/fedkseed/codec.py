@@ -1,0 +1,189 @@
+"""Host side of the MI355X FedKSeed codec: torch tensors in, libfks.so calls out.
+
+Three operations, each replacing one reference routine (include/fks.h has the ABI):
+
+* ``directional_step``  -- K x zo_utils.directional_derivative_step
+  (python/fate_llm/algo/fedkseed/zo_utils.py:23-54); K = 1 is the local ZO update
+  (optimizer.py:92), K = len(seeds) the reconstruct loop of ClientTrainer.train_once
+  (fedkseed.py:136-141) in ONE device pass.
+* ``perturb``          -- ZerothOrderOptimizer.random_perturb_parameters
+  (optimizer.py:152-173).
+* ``normal_``          -- the torch.normal(mean=0, std=1, size, dtype) draws the two
+  routines above make after torch.manual_seed(seed) (zo_utils.py:47, optimizer.py:170).
+
+The z stream is the one the reference produces on CPU tensors (torch's mt19937 +
+normal_fill), regenerated on the GPU; updates are applied in place (the reference
+rebinds ``param.data`` to a new tensor of identical values).
+
+There is no CPU path: tensors must live on a HIP device and libfks.so must be
+loadable, otherwise these functions raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+_DTYPES = {torch.float32: N.F32, torch.bfloat16: N.BF16, torch.float16: N.F16}
+
+
+@dataclass
+class ParamSpec:
+    """One tensor of the z stream, in draw order."""
+
+    tensor: torch.Tensor
+    lr: float = 0.0
+    weight_decay: Optional[float] = None  # None -> zo_utils.py:52 form (no decay term)
+    frozen: bool = False                  # draws its z, is not written
+
+
+def _f32(x: float) -> float:
+    return float(np.float32(x))
+
+
+class _Batch:
+    """fks_tensor array for a list of specs (keeps contiguous staging copies alive)."""
+
+    def __init__(self, specs: Sequence[ParamSpec]):
+        self.specs = list(specs)
+        self.copies = []  # (original, contiguous staging) pairs to write back
+        self.device = None
+        arr = (N.FksTensor * max(1, len(self.specs)))()
+        for i, sp in enumerate(self.specs):
+            t = sp.tensor
+            if t.dtype not in _DTYPES:
+                raise NotImplementedError(f"FedKSeed codec: dtype {t.dtype} is not supported on the MI355X path")
+            if t.device.type != "cuda":
+                raise ValueError("FedKSeed codec: parameters must be on a HIP device "
+                                 f"(got {t.device}); there is no CPU path")
+            if self.device is None:
+                self.device = t.device
+            elif t.device != self.device:
+                raise ValueError("FedKSeed codec: all parameters must be on one device")
+            if not t.is_contiguous():
+                c = t.contiguous()
+                self.copies.append((t, c))
+                t = c
+            arr[i].data = t.data_ptr() if t.numel() else None
+            arr[i].numel = t.numel()
+            arr[i].dtype = _DTYPES[t.dtype]
+            flags = 0
+            if sp.weight_decay is not None:
+                flags |= N.HAS_WD
+            if sp.frozen:
+                flags |= N.FROZEN
+            arr[i].flags = flags
+            arr[i].lr = _f32(sp.lr)
+            arr[i].wd = _f32(sp.weight_decay) if sp.weight_decay is not None else 0.0
+        self.arr = arr
+        self.n = len(self.specs)
+
+    def workspace(self, k: int):
+        L = N.load()
+        nbytes = ctypes.c_size_t(0)
+        N.check(L.fks_workspace_size(ctypes.addressof(self.arr), self.n, int(k), ctypes.byref(nbytes)))
+        ws = torch.empty(max(int(nbytes.value), 1), dtype=torch.uint8, device=self.device)
+        return ws, int(nbytes.value)
+
+    def finish(self):
+        for orig, c in self.copies:
+            orig.copy_(c)
+
+
+def _stream_handle(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _seed_u64(s) -> int:
+    s = int(s)
+    if s < 0:
+        s &= 0xFFFFFFFFFFFFFFFF  # torch.manual_seed accepts negatives as two's complement
+    if s >= 1 << 64:
+        raise ValueError(f"seed {s} out of range")
+    return s
+
+
+def directional_step(specs: Sequence[ParamSpec], seeds: Sequence[int], values: Sequence[float],
+                     value_is_tensor: bool = False) -> None:
+    """For each (seed, value) in order: p <- p - lr*(value*z + wd*p) over ``specs``."""
+    if len(seeds) != len(values):
+        raise ValueError("seeds and values differ in length")
+    if not specs or not len(seeds):
+        return
+    b = _Batch(specs)
+    if b.device is None:
+        return
+    L = N.load()
+    s = np.ascontiguousarray([_seed_u64(x) for x in seeds], dtype=np.uint64)
+    v = np.ascontiguousarray([float(x) for x in values], dtype=np.float64)
+    with torch.cuda.device(b.device):
+        ws, nbytes = b.workspace(len(s))
+        N.check(L.fks_directional_step(ctypes.addressof(b.arr), b.n, s.ctypes.data, v.ctypes.data, len(s),
+                                       N.VALUE_TENSOR if value_is_tensor else N.VALUE_SCALAR,
+                                       ws.data_ptr(), nbytes, _stream_handle(b.device)))
+        b.finish()
+
+
+def perturb(tensors: Sequence[torch.Tensor], seed: int, scales) -> None:
+    """p <- p + scale_i*z for every tensor i (scale = scaling_factor*eps of its group, a
+    python double); ``scales`` is one number for all tensors or one per tensor."""
+    specs = [ParamSpec(t) for t in tensors]
+    if not specs:
+        return
+    if isinstance(scales, (int, float)):
+        scales = [float(scales)] * len(specs)
+    if len(scales) != len(specs):
+        raise ValueError("one scale per tensor")
+    b = _Batch(specs)
+    if b.device is None:
+        return
+    L = N.load()
+    sc = np.ascontiguousarray([float(x) for x in scales], dtype=np.float64)
+    with torch.cuda.device(b.device):
+        ws, nbytes = b.workspace(1)
+        N.check(L.fks_perturb(ctypes.addressof(b.arr), b.n, _seed_u64(seed), sc.ctypes.data, ws.data_ptr(), nbytes,
+                              _stream_handle(b.device)))
+        b.finish()
+
+
+def normal_(tensors: Sequence[torch.Tensor], seed: int, frozen: Optional[Sequence[bool]] = None) -> None:
+    """Overwrite every tensor with the z the reference draws for it after manual_seed(seed)."""
+    specs = [ParamSpec(t, frozen=bool(frozen[i]) if frozen else False) for i, t in enumerate(tensors)]
+    if not specs:
+        return
+    b = _Batch(specs)
+    if b.device is None:
+        return
+    L = N.load()
+    with torch.cuda.device(b.device):
+        ws, nbytes = b.workspace(1)
+        N.check(L.fks_normal(ctypes.addressof(b.arr), b.n, _seed_u64(seed), ws.data_ptr(), nbytes,
+                             _stream_handle(b.device)))
+        b.finish()
+
+
+def resolve_groups(param_groups: List[dict], lr=None, weight_decay=None) -> List[ParamSpec]:
+    """zo_utils.py:43-46: walk the groups in order; lr / weight_decay are re-bound from
+    each group only while still None -- so the first group's values stick for all
+    later groups ("sticky" semantics)."""
+    specs = []
+    for group in param_groups:
+        weight_decay = group["weight_decay"] if weight_decay is None else weight_decay
+        lr = group["lr"] if lr is None else lr
+        for p in group["params"]:
+            specs.append(ParamSpec(p.data, lr=float(lr) if lr is not None else 0.0,
+                                   weight_decay=None if weight_decay is None else float(weight_decay)))
+    return specs
+
+
+def is_finite_number(x) -> bool:
+    try:
+        return math.isfinite(float(x))
+    except (TypeError, ValueError):
+        return False

@@ -1,0 +1,127 @@
+"""Drop-in for python/fate_llm/algo/fedkseed/optimizer.py (FATE-LLM 2.2.0).
+
+MeZO-style zeroth-order optimizers with the K-seed sampler of FedKSeed.  Class
+names, constructor arguments, methods and return conventions follow the reference
+(RandomWalkOptimizer :55-99, ZerothOrderOptimizer :102-173,
+KSeedZerothOrderOptimizer :176-235).  The two N-sized operations -- the +-eps*z
+perturbations and the directional update -- run on the MI355X codec.
+"""
+import math
+from typing import Callable, List, Mapping, Optional, Tuple
+
+import torch
+from torch.optim import Optimizer
+
+from . import codec
+from .pytorch_utils import get_optimizer_parameters_grouped_with_decay
+from .zo_utils import directional_derivative_step
+
+
+class RandomWalkOptimizer(Optimizer):
+    """Updates parameters along a seeded random direction (no gradients)."""
+
+    def __init__(self, params, lr, weight_decay, grad_clip, defaults=None):
+        self.lr = lr
+        self.weight_decay = weight_decay
+        self.grad_clip = grad_clip
+        merged = dict(defaults) if defaults is not None else {}
+        merged.update(lr=lr, weight_decay=weight_decay)
+        super().__init__(params, merged)
+
+    @classmethod
+    def from_model(cls, model, lr, weight_decay, grad_clip, **kwargs):
+        groups = get_optimizer_parameters_grouped_with_decay(model, weight_decay)
+        kwargs.update(lr=lr, weight_decay=weight_decay, grad_clip=grad_clip)
+        return cls(groups, **kwargs)
+
+    def directional_derivative_step(
+        self, directional_derivative_seed: int, directional_derivative_value: torch.FloatTensor
+    ) -> torch.FloatTensor:
+        """Apply the update unless |value| exceeds a positive grad_clip (then NaN, no update)."""
+        if self.grad_clip > 0.0 and abs(directional_derivative_value) > self.grad_clip:
+            return torch.FloatTensor([torch.nan])
+        directional_derivative_step(self.param_groups, directional_derivative_seed, directional_derivative_value)
+        return directional_derivative_value
+
+    def step(self, closure: Optional[Callable[[], float]] = None) -> Optional[float]:
+        raise NotImplementedError(
+            "use random_step instead of step for RandomWalkOptimizer "
+            "since we need pass the `seed` and `grad_projected_value`"
+        )
+
+
+class ZerothOrderOptimizer(RandomWalkOptimizer):
+    """Two-point (SPSA / MeZO) estimate of the directional derivative along z."""
+
+    def __init__(self, params, lr, eps, weight_decay, grad_clip):
+        self.eps = eps
+        super().__init__(params, lr, weight_decay, grad_clip, dict(eps=eps))
+
+    def zeroth_order_step(
+        self, directional_derivative_seed: int, closure: Callable[[], torch.FloatTensor]
+    ) -> Tuple[torch.FloatTensor, torch.FloatTensor, torch.FloatTensor]:
+        """x+eps*z -> loss_right; x-eps*z -> loss_left; back to x; then the update with
+        g = (loss_right - loss_left) / (2 eps).  Returns (g, loss_right, loss_left); a NaN
+        loss short-circuits before the update, as in the reference."""
+        self.random_perturb_parameters(directional_derivative_seed, scaling_factor=1.0)
+        loss_right = closure()
+        self.random_perturb_parameters(directional_derivative_seed, scaling_factor=-2.0)
+        loss_left = closure()
+        self.random_perturb_parameters(directional_derivative_seed, scaling_factor=1.0)
+
+        if torch.isnan(loss_right):
+            return loss_right, loss_right, loss_left
+        if torch.isnan(loss_left):
+            return loss_left, loss_right, loss_left
+
+        g = (loss_right - loss_left) / (2 * self.eps)
+        g = self.directional_derivative_step(directional_derivative_seed, g)
+        return g, loss_right, loss_left
+
+    def random_perturb_parameters(self, directional_derivative_seed: int, scaling_factor: float):
+        """p <- p + scaling_factor*eps*z for every parameter that requires grad; frozen
+        parameters draw no z (their stream slot is skipped, as in the reference)."""
+        torch.manual_seed(directional_derivative_seed)
+        tensors, scales = [], []
+        for group in self.param_groups:
+            scale = scaling_factor * group["eps"]  # python double, cast to fp32 at the multiply
+            for p in group["params"]:
+                if p.requires_grad:
+                    tensors.append(p.data)
+                    scales.append(scale)
+        codec.perturb(tensors, directional_derivative_seed, scales)
+
+
+class KSeedZerothOrderOptimizer(ZerothOrderOptimizer):
+    """Zeroth-order optimizer that samples its direction seed from K candidates and
+    records the directional derivative observed for each seed."""
+
+    def __init__(self, params, seed_candidates: torch.LongTensor, seed_probabilities: torch.FloatTensor,
+                 lr, eps, weight_decay, grad_clip):
+        self.seed_candidate = seed_candidates
+        self.seed_probabilities = seed_probabilities
+        self.directional_derivative_history: Mapping[int, List[float]] = {s.item(): [] for s in seed_candidates}
+        self.sample_random_generator = torch.Generator()  # unseeded, as in the reference (optimizer.py:190)
+        super().__init__(params, lr, eps, weight_decay, grad_clip)
+
+    def sample(self) -> int:
+        idx = torch.multinomial(input=self.seed_probabilities, num_samples=1,
+                                generator=self.sample_random_generator)[0].item()
+        return self.seed_candidate[idx].item()
+
+    def step(self, closure: Callable[[], torch.FloatTensor] = None) -> torch.FloatTensor:
+        if closure is None:
+            # HF Trainer calls step() without a closure after training_step; no-op (NaN)
+            return torch.FloatTensor([torch.nan])
+        return self.kseed_zeroth_order_step(closure)
+
+    def kseed_zeroth_order_step(self, closure: Callable[[], torch.FloatTensor]) -> torch.FloatTensor:
+        """Sample a seed, run the zeroth-order step, record g for that seed; returns loss_right."""
+        if closure is None:
+            raise ValueError("closure must not be None")
+        seed = self.sample()
+        g, loss_right, loss_left = self.zeroth_order_step(seed, closure)
+        if math.isnan(g):
+            return g
+        self.directional_derivative_history[seed].append(g.item())
+        return loss_right

@@ -1,0 +1,206 @@
+"""GPU parity of the HIP product path (libfks.so through the drop-in API) against the
+CPU oracle and the reference's golden vectors.
+
+Bar: bit-exact (NaN matches NaN) for fp32 and bf16 -- the z stream is integer/table
+work plus op-for-op restated float arithmetic, so there is nothing to tolerate.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import as_float, assert_bitwise
+from oracle import fks_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DTC = {"float32": O.F32, "bfloat16": O.BF16}
+TD = {"float32": torch.float32, "bfloat16": torch.bfloat16}
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+def to_np(t: torch.Tensor) -> np.ndarray:
+    t = t.detach().contiguous().cpu()
+    if t.dtype == torch.bfloat16:
+        return t.view(torch.int16).numpy().view(np.uint16).copy()
+    return t.numpy().copy()
+
+
+def from_np(a: np.ndarray, dtype: str, dev) -> torch.Tensor:
+    if dtype == "bfloat16":
+        return torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16).to(dev)
+    return torch.from_numpy(a.copy()).to(dev)
+
+
+def rand_params(shapes, dtype, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return [to_np((torch.randn(n, generator=g) * 0.02).to(TD[dtype])) for n in shapes]
+
+
+# ----------------------------------------------------------------------------- z streams
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("seed", [0, 7, 2**32 - 1, 3141592653, 2**40 + 3])
+def test_normal_stream_matches_oracle(dtype, seed):
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    shapes = [16, 64, 624, 1248, 4096, 100000, 32, 2**18 + 48]
+    ts = [torch.empty(n, dtype=TD[dtype], device=dev) for n in shapes]
+    codec.normal_(ts, seed)
+    gen = O.Generator(seed)
+    for n, t in zip(shapes, ts):
+        assert_bitwise(to_np(t), gen.normal(n, DTC[dtype]), dtype, f"seed {seed} n {n}")
+
+
+@pytest.mark.parametrize("dtype,key", [("float32", "long_float32"), ("bfloat16", "long_bfloat16")])
+def test_normal_stream_matches_golden(golden, dtype, key):
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    ref = golden("normal_streams.npz")[key]
+    t = torch.empty(ref.size, dtype=TD[dtype], device=dev)
+    codec.normal_([t], 2024)
+    assert_bitwise(to_np(t), ref, dtype, key)
+
+
+# ----------------------------------------------------------------------------- reconstruct
+def _gpu_reconstruct(arrays, dtype, lrs, wds, seeds, scalars, tensor_value=False):
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    ts = [from_np(a, dtype, dev) for a in arrays]
+    specs = [codec.ParamSpec(t, lr=lr, weight_decay=wd) for t, lr, wd in zip(ts, lrs, wds)]
+    codec.directional_step(specs, list(seeds), list(scalars), value_is_tensor=tensor_value)
+    torch.cuda.synchronize()
+    return [to_np(t) for t in ts]
+
+
+REGULAR_CASES = ["f32_wd", "f32_nowd", "bf16_wd", "bf16_nowd", "f32_sticky", "bf16_sticky", "f32_edge", "bf16_nan",
+                 "f32_wdnone"]
+
+
+@pytest.mark.parametrize("name", REGULAR_CASES)
+def test_reconstruct_golden(golden, cases, name):
+    """The train_once reconstruct loop through the drop-in zo_utils, vs the reference."""
+    from fate_llm.algo.fedkseed import zo_utils
+    dev = _dev()
+    case = cases["reconstruct"][name]
+    z = golden(f"reconstruct_{name}.npz")
+    order = [n for grp in case["groups"] for n in grp]
+    dt = case["dtype"]
+    params = {n: torch.nn.Parameter(from_np(z[f"init/{n}"].reshape(-1), dt, dev)) for n in order}
+    groups = [{"params": [params[n] for n in grp], "weight_decay": wd, "lr": lr}
+              for grp, wd, lr in zip(case["groups"], case["group_wd"], case["group_lr"])]
+    if case["sticky"]:
+        for s, g in zip(z["seeds"].tolist(), z["scalars"].tolist()):
+            if g != 0.0:
+                zo_utils.directional_derivative_step(groups, int(s), g)
+    else:
+        zo_utils.reconstruct_(groups, z["seeds"].tolist(), z["scalars"].tolist(), lr=case["lr"],
+                              weight_decay=case["wd"])
+    torch.cuda.synchronize()
+    for n in order:
+        assert_bitwise(to_np(params[n].data), z[f"final/{n}"], dt, f"{name}/{n}")
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_reconstruct_multichunk_vs_oracle(dtype):
+    """4M params in 7 tensors, K=61 (three seed passes), ~512 chunks: every chunk start is a
+    GF(2) jump; the full result must equal the oracle's sequential reconstruct bit for bit."""
+    shapes = [2**20, 48, 1234 * 16, 2**21, 4096 * 3, 16, 2**19 + 4096]
+    arrays = rand_params(shapes, dtype, seed=1)
+    gg = torch.Generator().manual_seed(5)
+    seeds = torch.randint(0, 2**32, (61,), generator=gg).tolist()
+    vals = (torch.randn(61, generator=gg, dtype=torch.float64) * 20).tolist()
+    lrs = [1e-3] * len(shapes)
+    wds = [0.01, 0.0, 0.01, None, 0.01, 0.01, 0.0]
+    got = _gpu_reconstruct(arrays, dtype, lrs, wds, seeds, vals)
+    O.reconstruct(arrays, [DTC[dtype]] * len(arrays), lrs, wds, seeds, vals)
+    for i, (a, b) in enumerate(zip(got, arrays)):
+        assert_bitwise(a, b, dtype, f"tensor {i}")
+
+
+def test_mixed_dtype_stream():
+    """fp32 and bf16 tensors interleaved in one stream: each dtype pass must keep the
+    other dtype's stream positions."""
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    shapes = [4096, 624 * 16, 2**16, 160, 2**15]
+    dts = ["float32", "bfloat16", "float32", "bfloat16", "bfloat16"]
+    arrays = [rand_params([n], d, seed=i)[0] for i, (n, d) in enumerate(zip(shapes, dts))]
+    seeds, vals = [11, 22, 33], [3.5, -7.25, 100.0]
+    ts = [from_np(a, d, dev) for a, d in zip(arrays, dts)]
+    specs = [codec.ParamSpec(t, lr=1e-3, weight_decay=0.01) for t in ts]
+    codec.directional_step(specs, seeds, vals)
+    O.reconstruct(arrays, [DTC[d] for d in dts], [1e-3] * 5, [0.01] * 5, seeds, vals)
+    for i, (t, a, d) in enumerate(zip(ts, arrays, dts)):
+        assert_bitwise(to_np(t), a, d, f"tensor {i}")
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_edge_values(dtype):
+    """Denormals, zeros of both signs, infinities and NaNs in the parameters; huge,
+    tiny, negative-zero and NaN directional values."""
+    n = 4096
+    base = rand_params([n], dtype, seed=3)[0]
+    f = as_float(base, dtype).astype(np.float32)
+    f[:8] = [0.0, -0.0, np.inf, -np.inf, np.nan, 1e-40, -1e-39, 3e38]
+    f[8:16] = np.float32(1.2e-38) * np.arange(8, dtype=np.float32)
+    arr = f if dtype == "float32" else to_np(torch.from_numpy(f).to(torch.bfloat16))
+    seeds = [1, 2, 3, 4, 5, 6]
+    vals = [1e30, -0.0, 1e-45, float("nan"), 5.0, -3e38]
+    got = _gpu_reconstruct([arr], dtype, [1e-2], [0.5], seeds, vals)
+    O.reconstruct([arr], [DTC[dtype]], [1e-2], [0.5], seeds, vals)
+    assert_bitwise(got[0], arr, dtype, "edge")
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_tensor_valued_step_rounds_value_to_param_dtype(dtype):
+    """zeroth_order_step passes g as a 0-dim fp32 tensor, the FIRST operand of g*z: torch
+    casts it to the parameter dtype first (bf16 rounding)."""
+    arr = rand_params([2048], dtype, seed=4)[0]
+    g = float(np.float32(0.125) / np.float32(2 * 5e-4))
+    got = _gpu_reconstruct([arr], dtype, [1e-3], [0.0], [12345678], [g], tensor_value=True)
+    gg = g
+    if dtype == "bfloat16":
+        gg = float(torch.tensor(g, dtype=torch.float32).to(torch.bfloat16).float())
+    O.reconstruct([arr], [DTC[dtype]], [1e-3], [0.0], [12345678], [gg])
+    assert_bitwise(got[0], arr, dtype, "tensor-valued g")
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_perturb_sequence_vs_oracle(dtype):
+    """+1, -2, +1 perturbations (optimizer.py:128-136) on a regular layout, and the
+    per-group eps (mixed scales) path."""
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    shapes = [4800, 48, 48, 6912, 144, 6912, 48, 48]
+    arrays = rand_params(shapes, dtype, seed=6)
+    ts = [from_np(a, dtype, dev) for a in arrays]
+    eps = 5e-4
+    for sf in (1.0, -2.0, 1.0):
+        codec.perturb(ts, 987654321, sf * eps)
+        O.perturb_params(arrays, [DTC[dtype]] * len(arrays), 987654321, sf * eps)
+        for i, (t, a) in enumerate(zip(ts, arrays)):
+            assert_bitwise(to_np(t), a, dtype, f"sf {sf} tensor {i}")
+    scales = [1e-3 if i % 2 else 5e-4 for i in range(len(ts))]
+    codec.perturb(ts, 42, scales)
+    gen = O.Generator(42)
+    for i, (t, a) in enumerate(zip(ts, arrays)):
+        zz = gen.normal(a.size, DTC[dtype])
+        O.perturb(a, zz, DTC[dtype], scales[i])
+        assert_bitwise(to_np(t), a, dtype, f"mixed-eps tensor {i}")
+
+
+def test_zeroth_order_optimizer_end_to_end():
+    """KSeedZerothOrderOptimizer steps with a device-independent closure, vs the golden
+    run of the reference optimizer on CPU (regular layout only: float32 TinyLM)."""
+    pytest.skip("golden optimizer fixtures use a ragged layout; covered once the generic path lands")
+
+
+def test_cpu_tensors_rejected():
+    from fate_llm.algo.fedkseed import codec
+    _dev()
+    with pytest.raises(ValueError):
+        codec.normal_([torch.empty(32)], 1)
