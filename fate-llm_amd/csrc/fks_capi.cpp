@@ -100,7 +100,7 @@ struct Plan {
 
 int plan_nchunks(int64_t stream_len) {
   const int64_t nblocks = std::max<int64_t>(1, (stream_len + kMtN - 1) / kMtN);
-  const int64_t target = 2 * (int64_t)device_cu_count();  // two 320-thread workgroups per CU
+  const int64_t target = (int64_t)kApplyWgPerCu * device_cu_count();  // one wave of apply workgroups
   return (int)std::min<int64_t>(nblocks, target);
 }
 
@@ -197,7 +197,7 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
   hipError_t e = hipMemcpyAsync(ws, host.data(), W.header, hipMemcpyHostToDevice, (hipStream_t)stream);
   if (e != hipSuccess) throw Error(-FKS_EHIP, std::string("hipMemcpyAsync: ") + hipGetErrorString(e));
 
-  const int chunks_per_wg = std::max(1, std::min(8, P.nchunks));
+  const int chunks_per_wg = std::max(1, std::min(32, P.nchunks));  // 2 jumps per wave (16 waves)
   for (int s0 = 0; s0 < k; s0 += kMaxSeedsPerPass) {
     const int nb = std::min(kMaxSeedsPerPass, k - s0);
     JumpArgs ja{};

@@ -28,22 +28,36 @@ __device__ __forceinline__ uint32_t mt_twist(uint32_t u, uint32_t v) {
   return (((u & 0x80000000u) | (v & 0x7fffffffu)) >> 1) ^ ((v & 1u) ? kMatrixA : 0u);
 }
 
-// tempering, MT19937RNGEngine.h:141-145
+// v_bitop3_b32 truth tables (LOP3 convention: f(0xF0, 0xCC, 0xAA))
+constexpr unsigned kXorAnd = 0x78;  // a ^ (b & c)
+constexpr unsigned kXorMask = 0x28; // (a ^ b) & c
+
+// tempering, MT19937RNGEngine.h:141-145; each "y ^= (y << s) & M" is one shift + one bitop3
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
   y ^= (y >> 11);
-  y ^= (y << 7) & 0x9d2c5680u;
-  y ^= (y << 15) & 0xefc60000u;
+  y = __builtin_amdgcn_bitop3_b32(y, y << 7, 0x9d2c5680u, kXorAnd);
+  y = __builtin_amdgcn_bitop3_b32(y, y << 15, 0xefc60000u, kXorAnd);
   y ^= (y >> 18);
   return y;
 }
 
-// LDS word swizzle: flips bit 3 when bit 5 is set, so the 32 words a half-wave
-// reads in the pair phase ({16b + r}, b in 0..3, r in 0..7) hit 32 distinct banks.
-__device__ __forceinline__ int swz(int i) { return i ^ (((i >> 5) & 1) << 3); }
+// low 8 bits of the tempered word (the bf16 uniform), times 4 (a byte offset into a
+// 256-entry f32 table): ((y ^ (y >> 18)) & 0xFF) << 2 = ((y << 2) ^ (y >> 16)) & 0x3FC
+__device__ __forceinline__ uint32_t mt_temper_u8x4(uint32_t y) {
+  y ^= (y >> 11);
+  y = __builtin_amdgcn_bitop3_b32(y, y << 7, 0x9d2c5680u, kXorAnd);
+  y = __builtin_amdgcn_bitop3_b32(y, y << 15, 0xefc60000u, kXorAnd);
+  return __builtin_amdgcn_bitop3_b32(y << 2, y >> 16, 0x3FCu, kXorMask);
+}
 
 // ------------------------------------------------------------------ rounding
-__device__ __forceinline__ float rbf(float x) {  // RNE to bf16 and back (v_cvt_pk_bf16_f32)
-  return static_cast<float>(static_cast<__bf16>(x));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+// RNE to bf16, result kept as the f32 with the same value: ONE v_cvt_pk_bf16_f32 with
+// a zero low half (hi = bf16(x), lo = bf16(0) = 0x0000).  NaN stays NaN.
+__device__ __forceinline__ float rbf(float x) {
+  const f32x2_t v = {0.0f, x};
+  return __builtin_bit_cast(float, __builtin_convertvector(v, bf16x2_t));
 }
 __device__ __forceinline__ float rhf(float x) {  // RNE to f16 and back
   return static_cast<float>(static_cast<_Float16>(x));
@@ -137,33 +151,32 @@ __device__ __forceinline__ void z_pair_f32(uint32_t w1, uint32_t w2, float& z1, 
 template <int DT>
 struct Traits;
 
+typedef __attribute__((address_space(1))) float gf32;
+typedef __attribute__((address_space(1))) uint16_t gu16;
+typedef __attribute__((address_space(1))) _Float16 gf16;
+
 template <>
 struct Traits<FKS_F32> {
-  using T = float;
-  __device__ static float load(const void* p, int64_t i) { return reinterpret_cast<const float*>(p)[i]; }
-  __device__ static void store(void* p, int64_t i, float v) { reinterpret_cast<float*>(p)[i] = v; }
+  __device__ static float load(uint64_t p, int64_t i) { return reinterpret_cast<const gf32*>(p)[i]; }
+  __device__ static void store(uint64_t p, int64_t i, float v) { reinterpret_cast<gf32*>(p)[i] = v; }
   __device__ static float rnd(float x) { return x; }
 };
 
 template <>
 struct Traits<FKS_BF16> {
-  __device__ static float load(const void* p, int64_t i) {
-    return __uint_as_float((uint32_t)reinterpret_cast<const uint16_t*>(p)[i] << 16);
+  __device__ static float load(uint64_t p, int64_t i) {
+    return __uint_as_float((uint32_t)reinterpret_cast<const gu16*>(p)[i] << 16);
   }
-  __device__ static void store(void* p, int64_t i, float v) {  // v is bf16-exact
-    reinterpret_cast<uint16_t*>(p)[i] = (uint16_t)(__float_as_uint(v) >> 16);
+  __device__ static void store(uint64_t p, int64_t i, float v) {  // v is bf16-exact
+    reinterpret_cast<gu16*>(p)[i] = (uint16_t)(__float_as_uint(v) >> 16);
   }
   __device__ static float rnd(float x) { return rbf(x); }
 };
 
 template <>
 struct Traits<FKS_F16> {
-  __device__ static float load(const void* p, int64_t i) {
-    return static_cast<float>(reinterpret_cast<const _Float16*>(p)[i]);
-  }
-  __device__ static void store(void* p, int64_t i, float v) {
-    reinterpret_cast<_Float16*>(p)[i] = static_cast<_Float16>(v);
-  }
+  __device__ static float load(uint64_t p, int64_t i) { return static_cast<float>(reinterpret_cast<const gf16*>(p)[i]); }
+  __device__ static void store(uint64_t p, int64_t i, float v) { reinterpret_cast<gf16*>(p)[i] = static_cast<_Float16>(v); }
   __device__ static float rnd(float x) { return rhf(x); }
 };
 
@@ -173,9 +186,10 @@ template <int DT>
 __device__ __forceinline__ float apply_one(float p, float z, float g, float lr, float wd, bool has_wd, int mode) {
   using TR = Traits<DT>;
   if (mode == kModeUpdate) {
-    float t = TR::rnd(g * z);                 // directional_derivative_value * z
-    if (has_wd) t = TR::rnd(t + TR::rnd(wd * p));  // + weight_decay * param.data
-    return TR::rnd(p - TR::rnd(lr * t));      // param.data - lr * (...)
+    const float gz = TR::rnd(g * z);                    // directional_derivative_value * z
+    const float t2 = TR::rnd(gz + TR::rnd(wd * p));     // + weight_decay * param.data
+    const float t = has_wd ? t2 : gz;                   // (select: keeps the seed loop branch-free)
+    return TR::rnd(p - TR::rnd(lr * t));                // param.data - lr * (...)
   } else if (mode == kModePerturb) {           // lr carries f32(scaling_factor * eps) here
     return TR::rnd(p + TR::rnd(lr * z));      // param.data + scaling_factor * eps * z
   }
@@ -183,11 +197,24 @@ __device__ __forceinline__ float apply_one(float p, float z, float g, float lr, 
 }
 
 // ------------------------------------------------------------------ jump kernel
-// grid (ceil(nchunks / chunks_per_wg), nseeds); block kJumpThreads; LDS kJumpXLen words.
+// grid (nseeds, ceil(nchunks / chunks_per_wg)); block kJumpThreads (8 waves).
+// LDS holds the seed's x[0..20560] (+ slack read by the last sliding window) at a
+// 3-word offset, so that y = x + 1 is 16-byte aligned.  Each wave evaluates the jump
+// of one chunk at a time: lane l < 52 owns window words w = 12l .. 12l+11 and sweeps
+// the 19937 coefficients of c(t) = t^J mod phi four at a time, keeping
+// y[i + 12l .. i + 12l + 15] in a 16-register sliding window fed by one ds_read_b128
+// per step:  acc[j] ^= y[i + d + 12l + j] & -c[i + d]   (d = 0..3, j = 0..11).
+constexpr int kJumpLanes = 52;          // 52 lanes x 12 words = 624
+constexpr int kJumpXOff = 3;            // x at word 3 -> y = x + 1 at word 4 (16 B aligned)
+constexpr int kJumpLdsWords = kJumpXOff + kJumpXLen + 64;  // + over-read slack of the last window
+
+__device__ __forceinline__ uint4 lds_b128(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
 __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t xs[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_j[];
+  uint32_t* xs = lds_j + kJumpXOff;
   const int tid = threadIdx.x;
-  const int k = blockIdx.y;
+  const int k = blockIdx.x;
   const uint64_t seed = a.seeds[k];
   // mt19937::init_with_uint32 (MT19937RNGEngine.h:156-162): a serial recurrence
   if (tid == 0) {
@@ -198,6 +225,7 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
       xs[j] = s;
     }
   }
+  for (int j = kJumpXLen + tid; j < kJumpLdsWords - kJumpXOff; j += kJumpThreads) xs[j] = 0u;
   __syncthreads();
   // x[n] = x[n-227] ^ twist(x[n-624], x[n-623]): 227 independent words per step
   for (int base = kMtN; base < kJumpXLen; base += kMtN - kMtM) {
@@ -205,127 +233,225 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
     if (tid < kMtN - kMtM && n < kJumpXLen) xs[n] = xs[n - (kMtN - kMtM)] ^ mt_twist(xs[n - kMtN], xs[n - kMtN + 1]);
     __syncthreads();
   }
-  const int c0 = blockIdx.x * a.chunks_per_wg;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const uint32_t* yb = xs + 1 + 12 * lane;  // y[12 lane]
+  const int c0 = blockIdx.y * a.chunks_per_wg;
   const int c1 = min(c0 + a.chunks_per_wg, a.nchunks);
-  const int w = tid;
-  for (int c = c0; c < c1; c++) {
+  for (int c = c0 + wave; c < c1; c += kJumpThreads / 64) {
     const int64_t b = a.chunk_block[c];
-    uint32_t acc = 0;
-    if (b == 0) {
-      if (w < kMtN) acc = xs[w];
-    } else {
-      const uint64_t* poly = a.polys + (size_t)c * 312;
-      const uint32_t* yb = xs + 1 + w;  // y[i + w] = x[i + w + 1]
-      for (int wd = 0; wd < 312; wd++) {
-        uint64_t bits = poly[wd];
-        const int i0 = wd * 64;
-        while (bits) {
-          const int i = i0 + __builtin_ctzll(bits);
-          bits &= bits - 1;
-          if (w < kMtN) acc ^= yb[i];
+    uint32_t acc[12];
+#pragma unroll
+    for (int j = 0; j < 12; j++) acc[j] = 0u;
+    if (lane < kJumpLanes) {
+      if (b == 0) {
+#pragma unroll
+        for (int j = 0; j < 12; j++) acc[j] = xs[12 * lane + j];
+      } else {
+        const uint64_t* poly = a.polys + (size_t)c * 312;  // wave-uniform: scalar loads
+        uint32_t win[16];
+        {
+          const uint4 q0 = lds_b128(yb), q1 = lds_b128(yb + 4), q2 = lds_b128(yb + 8);
+          win[0] = q0.x; win[1] = q0.y; win[2] = q0.z; win[3] = q0.w;
+          win[4] = q1.x; win[5] = q1.y; win[6] = q1.z; win[7] = q1.w;
+          win[8] = q2.x; win[9] = q2.y; win[10] = q2.z; win[11] = q2.w;
+          const uint4 q3 = lds_b128(yb + 12);
+          win[12] = q3.x; win[13] = q3.y; win[14] = q3.z; win[15] = q3.w;
+        }
+        uint64_t next = poly[0];
+        for (int wd = 0; wd < 312; wd++) {
+          const uint64_t bits = next;
+          if (wd + 1 < 312) next = poly[wd + 1];  // prefetch the next 64 coefficients
+          const uint32_t lo = (uint32_t)bits, hi = (uint32_t)(bits >> 32);
+          const uint32_t* yw = yb + 64 * wd;
+#pragma unroll
+          for (int q = 0; q < 16; q++) {
+            // window = y[64 wd + 4q + 12 lane + 0..15], stored rotated by 4q (mod 16)
+            const uint4 nx = lds_b128(yw + 4 * q + 16);
+            const int rot = (4 * q) & 15;
+            const uint32_t word = q < 8 ? lo : hi;
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+              // all-ones if coefficient 64 wd + 4q + d is set (scalar bit-field extract)
+              const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)word, (4 * q + d) & 31, 1);
+#pragma unroll
+              for (int j = 0; j < 12; j++) acc[j] = __builtin_amdgcn_bitop3_b32(acc[j], win[(rot + j + d) & 15], m, kXorAnd);
+            }
+            win[(rot + 0) & 15] = nx.x;
+            win[(rot + 1) & 15] = nx.y;
+            win[(rot + 2) & 15] = nx.z;
+            win[(rot + 3) & 15] = nx.w;
+          }
         }
       }
+      uint32_t* out = a.states + ((size_t)k * a.nchunks + c) * kMtN + 12 * lane;
+#pragma unroll
+      for (int j = 0; j < 12; j += 4) *reinterpret_cast<uint4*>(out + j) = make_uint4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
     }
-    if (w < kMtN) a.states[((size_t)k * a.nchunks + c) * kMtN + w] = acc;
   }
 }
 
 // ------------------------------------------------------------------ apply kernel
 // In-place twist of nseeds windows (MT19937RNGEngine.h:164-175).  Word i of the new
 // block needs OLD words i and i+1 plus word i+397 (old, i < 227) or i-227 (new), so
-// the 624 words form 3 dependency phases [0,227) [227,454) [454,624).  Within a
-// phase thread T walks a contiguous run of L items in ascending order (L odd, so
-// the 64 lanes hit distinct LDS banks): it reads old word i+1 before writing word
-// i+1 itself, and only the old word just past its run -- written by thread T+1 --
-// is read up front; a barrier then separates those reads (and every lane's reads
-// of the previous block) from the first write.  Word 623 pairs with the NEW word 0
-// (MT19937RNGEngine.h:174).
-__device__ __forceinline__ void twist_all(uint32_t* st, int nseeds, int tid) {
-  int a[3], b[3], L[3];
-  uint32_t pre[3];
+// the 624 words form 3 dependency phases [0,227) [227,454) [454,624); word 623 pairs
+// with the NEW word 0 (MT19937RNGEngine.h:174).  Items are dealt round-robin over
+// the 320 threads; every phase reads into registers, barriers, then writes (word i
+// reads word i+1, which another thread writes in the same phase).  Item addresses
+// depend only on (thread, nseeds), so they are computed once per kernel and the
+// three reads use immediate offsets.
+constexpr int kR12 = (227 * kMaxSeedsPerPass + kApplyThreads - 1) / kApplyThreads;  // items / thread, phases 1-2
+constexpr int kR3 = (170 * kMaxSeedsPerPass + kApplyThreads - 1) / kApplyThreads;   // items / thread, phase 3
+
+struct TwistPlan {
+  int a12[kR12];   // byte offset of (window k, word i') for phases 1-2
+  int a3[kR3];     // byte offset of (window k, word i'') for phase 3 (word 454 + i'')
+  uint32_t last3;  // bit r: item r of phase 3 is word 623 (its partner is the NEW word 0)
+};
+
+// Items are dealt round-robin; an item past the last seed lands in a window that is
+// either unused in this pass or the spare window kMaxSeedsPerPass, so every item runs
+// unconditionally (no exec-masked branches, all LDS reads of a phase in flight at once).
+__device__ __forceinline__ void twist_plan(TwistPlan& P, int tid, int st_base) {
 #pragma unroll
-  for (int ph = 0; ph < 3; ph++) {
-    const int lo = ph == 0 ? 0 : (ph == 1 ? 227 : 454);
-    const int len = ph == 2 ? 170 : 227;
-    const int total = len * nseeds;
-    L[ph] = ((total + kApplyThreads - 1) / kApplyThreads) | 1;
-    a[ph] = tid * L[ph];
-    b[ph] = min(a[ph] + L[ph], total);
-    pre[ph] = 0;
-    if (a[ph] < b[ph]) {
-      const int last = b[ph] - 1;
-      const int k = last / len;
-      const int i = lo + (last - k * len);
-      if (i + 1 < kMtN) pre[ph] = st[k * kMtN + swz(i + 1)];
-    }
+  for (int r = 0; r < kR12; r++) {
+    const int it = tid + r * kApplyThreads;
+    const int k = it / 227, i = it - k * 227;
+    P.a12[r] = st_base + 4 * (min(k, kMaxSeedsPerPass) * kMtN + i);  // overflow items: spare window
+  }
+  P.last3 = 0;
+#pragma unroll
+  for (int r = 0; r < kR3; r++) {
+    const int it = tid + r * kApplyThreads;
+    const int k = it / 170, i = it - k * 170;
+    P.a3[r] = st_base + 4 * (min(k, kMaxSeedsPerPass) * kMtN + i);
+    if (i == 169) P.last3 |= 1u << r;
+  }
+}
+
+__device__ __forceinline__ uint32_t lds_u32(const uint8_t* base, int off) {
+  return *reinterpret_cast<const uint32_t*>(base + off);
+}
+__device__ __forceinline__ void lds_st(uint8_t* base, int off, uint32_t v) {
+  *reinterpret_cast<uint32_t*>(base + off) = v;
+}
+
+__device__ __forceinline__ void twist_all(uint8_t* lds, const TwistPlan& P) {
+  uint32_t nv[kR12];
+  // phase 1: words [0, 227): m = x[i + 397] (old)
+#pragma unroll
+  for (int r = 0; r < kR12; r++) {
+    const int o = P.a12[r];
+    nv[r] = lds_u32(lds, o + 4 * kMtM) ^ mt_twist(lds_u32(lds, o), lds_u32(lds, o + 4));
   }
   __syncthreads();
 #pragma unroll
-  for (int ph = 0; ph < 3; ph++) {
-    const int lo = ph == 0 ? 0 : (ph == 1 ? 227 : 454);
-    const int len = ph == 2 ? 170 : 227;
-    if (a[ph] < b[ph]) {
-      int k = a[ph] / len;
-      int i = lo + (a[ph] - k * len);
-      uint32_t* s = st + k * kMtN;
-      uint32_t u = s[swz(i)];
-      for (int it = a[ph]; it < b[ph]; it++) {
-        uint32_t v;
-        if (i == kMtN - 1) v = s[swz(0)];
-        else if (it == b[ph] - 1) v = pre[ph];
-        else v = s[swz(i + 1)];
-        const uint32_t m = s[swz(i < kMtN - kMtM ? i + kMtM : i - (kMtN - kMtM))];
-        s[swz(i)] = m ^ mt_twist(u, v);
-        i++;
-        if (i == lo + len) {
-          k++;
-          i = lo;
-          s = st + k * kMtN;
-          if (it + 1 < b[ph]) u = s[swz(i)];
-        } else {
-          u = v;
-        }
-      }
-    }
-    __syncthreads();
+  for (int r = 0; r < kR12; r++) lds_st(lds, P.a12[r], nv[r]);
+  __syncthreads();
+  // phase 2: words [227, 454): m = x[i - 227] (new, phase 1)
+#pragma unroll
+  for (int r = 0; r < kR12; r++) {
+    const int o = P.a12[r];
+    nv[r] = lds_u32(lds, o) ^ mt_twist(lds_u32(lds, o + 4 * 227), lds_u32(lds, o + 4 * 228));
   }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kR12; r++) lds_st(lds, P.a12[r] + 4 * 227, nv[r]);
+  __syncthreads();
+  // phase 3: words [454, 624): m = x[i - 227] (new, phase 2); word 623 pairs with new x[0]
+#pragma unroll
+  for (int r = 0; r < kR3; r++) {
+    const int o = P.a3[r];
+    const int ov = ((P.last3 >> r) & 1u) ? o - 4 * 169 - 4 * 455 : o;  // ov + 4*455 -> x[0] of this window
+    nv[r] = lds_u32(lds, o + 4 * 227) ^ mt_twist(lds_u32(lds, o + 4 * 454), lds_u32(lds, ov + 4 * 455));
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kR3; r++) lds_st(lds, P.a3[r] + 4 * 454, nv[r]);
+  __syncthreads();
 }
 
 __constant__ float c_tab_bf16[3 * 256];  // R | C | S, set once from fks::tables()
 
-template <int DT, int MODE>
-__global__ __launch_bounds__(kApplyThreads, 2) void fks_apply_kernel(ApplyArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* st = lds;                                                     // [nseeds][624], swizzled
-  float* gs = reinterpret_cast<float*>(lds + kMaxSeedsPerPass * kMtN);    // [kMaxSeedsPerPass]
-  float* tabR = gs + kMaxSeedsPerPass;                                    // bf16 radius R[a]
-  float2* tabCS = reinterpret_cast<float2*>(tabR + 256);                  // bf16 (C[b], S[b])
+// LDS: [R[256] f32 | (C,S)[256] f32x2 | windows (kMaxSeedsPerPass + 1) x 624 u32]
+constexpr int kLdsTabBytes = 256 * 4 + 256 * 8;
+constexpr int kLdsStBytes = (kMaxSeedsPerPass + 1) * kMtN * 4;
+
+// z pair of seed k for this lane's 16-block slot: raw words j1, j1+8 -> (z_j, z_{j+8})
+template <int DT>
+__device__ __forceinline__ void z_pair(const uint8_t* lds, uint32_t r1, uint32_t r2, float& z1, float& z2) {
+  if constexpr (DT == FKS_F32) {
+    z_pair_f32(mt_temper(r1), mt_temper(r2), z1, z2);
+  } else {
+    // normal_fill_16<BFloat16>: z = bf16(R[a] * C[b]) * 1 + 0 (std, mean).  R*C is exact
+    // in f32 (8-bit x 8-bit significands) and fma(R, C, +0) turns -0 into +0 like "+ mean".
+    const uint32_t a4 = mt_temper_u8x4(r1), b4 = mt_temper_u8x4(r2);
+    const float r = *reinterpret_cast<const float*>(lds + a4);
+    const float2 cs = *reinterpret_cast<const float2*>(lds + 1024 + 2 * b4);
+    z1 = rbf(__fmaf_rn(r, cs.x, 0.0f));
+    z2 = rbf(__fmaf_rn(r, cs.y, 0.0f));
+  }
+}
+
+// Seeds [k0, k0 + U): all LDS reads and z first (independent across seeds), then the
+// sequential per-element update chain in seed order.
+template <int DT, int MODE, int U>
+__device__ __forceinline__ void pair_group(const uint8_t* lds, int st_off, int k0, const float* g, float lr,
+                                           float wd, bool has_wd, float& p1, float& p2) {
+  uint32_t r1[U], r2[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    r1[u] = lds_u32(lds, st_off + (k0 + u) * (kMtN * 4));
+    r2[u] = lds_u32(lds, st_off + (k0 + u) * (kMtN * 4) + 32);
+  }
+  float z1[U], z2[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) z_pair<DT>(lds, r1[u], r2[u], z1[u], z2[u]);
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    p1 = apply_one<DT>(p1, z1[u], g[k0 + u], lr, wd, has_wd, MODE);
+    p2 = apply_one<DT>(p2, z2[u], g[k0 + u], lr, wd, has_wd, MODE);
+  }
+}
+
+template <int DT, int MODE, bool FULL>
+__global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255) / 256) void fks_apply_kernel(ApplyArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
   const int tid = threadIdx.x;
   const int c = blockIdx.x;
-  const int nseeds = a.nseeds;
+  const int nseeds = FULL ? kMaxSeedsPerPass : a.nseeds;
   const int64_t b0 = a.chunk_block[c], b1 = a.chunk_block[c + 1];
 
   if constexpr (DT == FKS_BF16) {
+    float* tabR = reinterpret_cast<float*>(lds);
+    float2* tabCS = reinterpret_cast<float2*>(lds + 1024);
     for (int i = tid; i < 256; i += kApplyThreads) {
       tabR[i] = c_tab_bf16[i];
       tabCS[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
     }
   }
-  if (tid < nseeds) gs[tid] = a.g[tid];
+  uint32_t* st = reinterpret_cast<uint32_t*>(lds + kLdsTabBytes);
   for (int idx = tid; idx < nseeds * kMtN; idx += kApplyThreads) {
     const int k = idx / kMtN, i = idx - k * kMtN;
-    st[k * kMtN + swz(i)] = a.states[((size_t)k * a.nchunks + c) * kMtN + i];
+    st[k * kMtN + i] = a.states[((size_t)k * a.nchunks + c) * kMtN + i];
   }
+  TwistPlan plan;
+  twist_plan(plan, tid, kLdsTabBytes);
+  // per-seed multipliers: wave-uniform, kept in SGPRs for the whole kernel
+  float gk[kMaxSeedsPerPass];
+#pragma unroll
+  for (int k = 0; k < kMaxSeedsPerPass; k++)
+    gk[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(k < nseeds ? a.g[k] : 0.0f)));
   __syncthreads();
 
   // Thread q < 312 owns Box-Muller pair q of every block: 16-block q/8, slot q%8,
   // i.e. block words j1 = 16*(q/8) + q%8 and j1 + 8 (DistributionTemplates.h:141-146).
   const bool lane_on = tid < kMtN / 2;
   const int j1 = 16 * (tid >> 3) + (tid & 7);
-  const int sj1 = swz(j1), sj2 = swz(j1 + 8);
+  const int st_off = kLdsTabBytes + 4 * j1;
 
-  // first segment that ends after this lane's first position
-  int cur = 0;
+  // The lane's current segment, cached in registers; positions only grow.
+  int cur;
   {
     const int64_t s1 = (int64_t)kMtN * b0 + j1;
     int lo = 0, hi = a.nsegs;
@@ -335,55 +461,74 @@ __global__ __launch_bounds__(kApplyThreads, 2) void fks_apply_kernel(ApplyArgs a
     }
     cur = lo;
   }
-
-  for (int64_t b = b0; b < b1; b++) {
-    twist_all(st, nseeds, tid);  // the words of stream block b, raw (untempered)
-    const int64_t s1 = (int64_t)kMtN * b + j1;
-    while (cur < a.nsegs && s1 >= a.segs[cur].start + a.segs[cur].numel) cur++;
-    if (lane_on && cur < a.nsegs && s1 >= a.segs[cur].start) {
-      const DevSeg* sg = a.segs + cur;
-      void* ptr = reinterpret_cast<void*>(sg->ptr);
-      const int64_t e1 = s1 - sg->start;
-      const float lr = sg->lr, wd = sg->wd;
-      const bool has_wd = (sg->flags & FKS_HAS_WD) != 0;
-      float p1 = 0.0f, p2 = 0.0f;
-      if (MODE != kModeWriteZ) {
-        p1 = Traits<DT>::load(ptr, e1);
-        p2 = Traits<DT>::load(ptr, e1 + 8);
-      }
-#pragma unroll 2
-      for (int k = 0; k < nseeds; k++) {
-        const uint32_t w1 = mt_temper(st[k * kMtN + sj1]);
-        const uint32_t w2 = mt_temper(st[k * kMtN + sj2]);
-        float z1, z2;
-        if constexpr (DT == FKS_F32) {
-          z_pair_f32(w1, w2, z1, z2);
-        } else {
-          // normal_fill_16<BFloat16>: z = bf16(R[a] * C[b]) * 1 + 0 (std, mean)
-          const float r = tabR[w1 & 0xFFu];
-          const float2 cs = tabCS[w2 & 0xFFu];
-          z1 = rbf(r * cs.x) + 0.0f;
-          z2 = rbf(r * cs.y) + 0.0f;
-        }
-        const float g = gs[k];
-        p1 = apply_one<DT>(p1, z1, g, lr, wd, has_wd, MODE);
-        p2 = apply_one<DT>(p2, z2, g, lr, wd, has_wd, MODE);
-      }
-      Traits<DT>::store(ptr, e1, p1);
-      Traits<DT>::store(ptr, e1 + 8, p2);
+  int64_t seg_start = INT64_MAX, seg_end = INT64_MAX;
+  uint64_t seg_ptr = 0;
+  float seg_lr = 0.0f, seg_wd = 0.0f;
+  bool seg_wdf = false;
+  auto load_seg = [&]() {
+    if (cur < a.nsegs) {
+      const DevSeg sg = a.segs[cur];
+      seg_start = sg.start;
+      seg_end = sg.start + sg.numel;
+      seg_ptr = sg.ptr;
+      seg_lr = sg.lr;
+      seg_wd = sg.wd;
+      seg_wdf = (sg.flags & FKS_HAS_WD) != 0;
+    } else {
+      seg_start = seg_end = INT64_MAX;
     }
-    // no barrier here: the next twist_all's first barrier orders these LDS reads
-    // before its first write
+  };
+  load_seg();
+
+  // software pipeline: block b+1's parameters are fetched before block b's Box-Muller
+  struct Slot { uint64_t ptr; int64_t e1; float lr, wd; bool wdf, on; float p1, p2; };
+  auto fetch = [&](int64_t b) {
+    Slot sl;
+    const int64_t s1 = (int64_t)kMtN * b + j1;
+    while (s1 >= seg_end) { cur++; load_seg(); }
+    sl.on = lane_on && s1 >= seg_start;
+    sl.ptr = seg_ptr; sl.e1 = s1 - seg_start; sl.lr = seg_lr; sl.wd = seg_wd; sl.wdf = seg_wdf;
+    sl.p1 = 0.0f; sl.p2 = 0.0f;
+    if (MODE != kModeWriteZ && sl.on) {
+      sl.p1 = Traits<DT>::load(sl.ptr, sl.e1);
+      sl.p2 = Traits<DT>::load(sl.ptr, sl.e1 + 8);
+    }
+    return sl;
+  };
+  Slot nxt = fetch(b0);
+
+#ifndef FKS_DIAG
+#define FKS_DIAG 0  // diagnostic builds only: 1 = twist only, 2 = Box-Muller/update only
+#endif
+  for (int64_t b = b0; b < b1; b++) {
+    Slot sl = nxt;
+    if (FKS_DIAG != 2) twist_all(lds, plan);  // the raw words of stream block b (sl's loads in flight meanwhile)
+    if (FKS_DIAG == 2) __syncthreads();
+    if (b + 1 < b1) nxt = fetch(b + 1);
+    if (sl.on && FKS_DIAG != 1) {
+      float p1 = sl.p1, p2 = sl.p2;
+      if constexpr (FULL) {
+#pragma unroll
+        for (int k0 = 0; k0 + 4 <= kMaxSeedsPerPass; k0 += 4)
+          pair_group<DT, MODE, 4>(lds, st_off, k0, gk, sl.lr, sl.wd, sl.wdf, p1, p2);
+        constexpr int kTail = kMaxSeedsPerPass % 4;
+        if constexpr (kTail > 0)
+          pair_group<DT, MODE, kTail>(lds, st_off, kMaxSeedsPerPass - kTail, gk, sl.lr, sl.wd, sl.wdf, p1, p2);
+      } else {
+        for (int k = 0; k < nseeds; k++) pair_group<DT, MODE, 1>(lds, st_off, k, gk, sl.lr, sl.wd, sl.wdf, p1, p2);
+      }
+      Traits<DT>::store(sl.ptr, sl.e1, p1);
+      Traits<DT>::store(sl.ptr, sl.e1 + 8, p2);
+    }
+    // no barrier here: the next twist's first barrier orders these LDS reads before
+    // its first write
   }
 }
 
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
-static size_t apply_lds_bytes() {
-  return sizeof(uint32_t) * (size_t)kMaxSeedsPerPass * kMtN + sizeof(float) * kMaxSeedsPerPass +
-         sizeof(float) * 256 + sizeof(float2) * 256;
-}
+static size_t apply_lds_bytes() { return (size_t)kLdsTabBytes + (size_t)kLdsStBytes; }
 
 int device_cu_count() {
   int dev = 0, n = 0;
@@ -409,7 +554,7 @@ static int ensure_tables() {
 }
 
 int launch_jump(const JumpArgs& a, int nseeds, void* stream) {
-  const size_t lds = sizeof(uint32_t) * (size_t)kJumpXLen;
+  const size_t lds = sizeof(uint32_t) * (size_t)kJumpLdsWords;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fks_jump_kernel),
@@ -417,24 +562,30 @@ int launch_jump(const JumpArgs& a, int nseeds, void* stream) {
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  dim3 grid((unsigned)((a.nchunks + a.chunks_per_wg - 1) / a.chunks_per_wg), (unsigned)nseeds);
+  dim3 grid((unsigned)nseeds, (unsigned)((a.nchunks + a.chunks_per_wg - 1) / a.chunks_per_wg));
   hipLaunchKernelGGL(fks_jump_kernel, grid, dim3(kJumpThreads), lds, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+template <int DT, int MODE, bool FULL>
+static int launch_apply_f(const ApplyArgs& a, void* stream) {
+  const size_t lds = apply_lds_bytes();
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fks_apply_kernel<DT, MODE, FULL>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((fks_apply_kernel<DT, MODE, FULL>), dim3((unsigned)a.nchunks), dim3(kApplyThreads), lds,
+                     (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 
 template <int DT, int MODE>
 static int launch_apply_t(const ApplyArgs& a, void* stream) {
-  const size_t lds = apply_lds_bytes();
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fks_apply_kernel<DT, MODE>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-    attr = true;
-  }
-  hipLaunchKernelGGL((fks_apply_kernel<DT, MODE>), dim3((unsigned)a.nchunks), dim3(kApplyThreads), lds,
-                     (hipStream_t)stream, a);
-  return (int)hipGetLastError();
+  return a.nseeds == kMaxSeedsPerPass ? launch_apply_f<DT, MODE, true>(a, stream)
+                                      : launch_apply_f<DT, MODE, false>(a, stream);
 }
 
 int launch_apply(int dtype, const ApplyArgs& a, void* stream) {

@@ -53,8 +53,13 @@ struct DevSeg {
 static_assert(sizeof(DevSeg) == 40, "DevSeg layout");
 
 constexpr int kApplyThreads = 320;  // 312 Box-Muller pairs per 624-word block + 8 idle lanes
-constexpr int kMaxSeedsPerPass = 28;  // MT states resident in LDS per workgroup (28 x 2496 B)
-constexpr int kJumpThreads = 640;
+#ifndef FKS_APPLY_WG_PER_CU
+#define FKS_APPLY_WG_PER_CU 3
+#endif
+constexpr int kApplyWgPerCu = FKS_APPLY_WG_PER_CU;  // resident apply workgroups per CU (LDS-limited)
+// MT windows resident in LDS per workgroup: (seeds + 1 spare) x 2496 B + 3 KB tables <= 160 KB / WGs
+constexpr int kMaxSeedsPerPass = (160 * 1024 / kApplyWgPerCu - 3072) / 2496 - 1;
+constexpr int kJumpThreads = 1024;  // 16 waves, one chunk's jump per wave at a time
 constexpr int kJumpXLen = 19937 + 624;  // x[0..20560]: y[i + w] = x[i + w + 1], i < 19937, w < 624
 
 enum ApplyMode : int { kModeUpdate = 0, kModePerturb = 1, kModeWriteZ = 2 };

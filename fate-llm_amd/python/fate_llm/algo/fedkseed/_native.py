@@ -11,7 +11,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfks.so")
+LIB_PATH = os.environ.get("FKS_LIB_OVERRIDE") or os.path.join(_HERE, "libfks.so")  # override: diagnostics only
 
 F32, BF16, F16 = 0, 1, 2
 HAS_WD, FROZEN = 1, 2
