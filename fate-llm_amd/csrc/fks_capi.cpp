@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -98,21 +99,47 @@ struct Plan {
   std::vector<uint64_t> polys;       // nchunks * 312
 };
 
-int plan_nchunks(int64_t stream_len) {
-  const int64_t nblocks = std::max<int64_t>(1, (stream_len + kMtN - 1) / kMtN);
-  const int64_t target = (int64_t)kApplyWgPerCu * device_cu_count();  // one wave of apply workgroups
-  return (int)std::min<int64_t>(nblocks, target);
+// MT blocks of the whole stream and the [lo, hi) range shard `shard` of `nshards` owns
+struct BlockRange { int64_t lo, hi; };
+BlockRange shard_blocks(int64_t stream_len, int shard, int nshards) {
+  const int64_t nb = std::max<int64_t>(1, (stream_len + kMtN - 1) / kMtN);
+  return {(int64_t)((__int128)nb * shard / nshards), (int64_t)((__int128)nb * (shard + 1) / nshards)};
 }
 
-Plan make_plan(int64_t stream_len) {
+int plan_nchunks(int64_t nblocks) {
+  const int64_t target = (int64_t)kApplyWgPerCu * device_cu_count();  // one wave of apply workgroups
+  return (int)std::max<int64_t>(1, std::min<int64_t>(nblocks, target));
+}
+
+Plan make_plan(BlockRange r) {
   Plan P;
-  const int64_t nblocks = std::max<int64_t>(1, (stream_len + kMtN - 1) / kMtN);
-  P.nchunks = plan_nchunks(stream_len);
+  const int64_t nblocks = std::max<int64_t>(1, r.hi - r.lo);
+  P.nchunks = plan_nchunks(nblocks);
   P.chunk_block.resize((size_t)P.nchunks + 1);
-  for (int c = 0; c <= P.nchunks; c++) P.chunk_block[(size_t)c] = (int64_t)((__int128)nblocks * c / P.nchunks);
+  for (int c = 0; c <= P.nchunks; c++)
+    P.chunk_block[(size_t)c] = r.lo + (int64_t)((__int128)nblocks * c / P.nchunks);
   std::vector<int64_t> starts(P.chunk_block.begin(), P.chunk_block.end() - 1);
   jump_polys_for_blocks(starts, P.polys);
   return P;
+}
+
+// keep only the part of every segment inside the block range (16-aligned cuts)
+void clip_segments(Layout& L, BlockRange r) {
+  const int64_t lo = r.lo * kMtN, hi = r.hi * kMtN;
+  for (int d = 0; d < 3; d++) {
+    std::vector<DevSeg> out;
+    for (const DevSeg& s : L.segs[d]) {
+      const int64_t a = std::max(s.start, lo), b = std::min(s.start + s.numel, hi);
+      if (a >= b) continue;
+      DevSeg c = s;
+      const size_t es = s.dtype == FKS_F32 ? 4 : 2;
+      c.ptr = s.ptr + (uint64_t)(a - s.start) * es;
+      c.start = a;
+      c.numel = b - a;
+      out.push_back(c);
+    }
+    L.segs[d].swap(out);
+  }
 }
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -154,9 +181,36 @@ inline float round_to_dtype(double v, int dtype) {
 }
 
 // Core: run `k` seeds (update / perturb / write-z) over the tensor list.
+// launch-time instrumentation (fks_profile_begin/end): events around every launch
+struct Prof {
+  bool on = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[2];  // 0 = apply, 1 = jump
+};
+Prof g_prof;
+std::mutex g_prof_mu;
+
+template <class F>
+int timed(int which, void* stream, F&& launch) {
+  std::unique_lock<std::mutex> lk(g_prof_mu);
+  if (!g_prof.on) {
+    lk.unlock();
+    return launch();
+  }
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipEventRecord(a, (hipStream_t)stream);
+  const int rc = launch();
+  hipEventRecord(b, (hipStream_t)stream);
+  g_prof.ev[which].emplace_back(a, b);
+  return rc;
+}
+
 void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* values, int k, int value_kind, int mode,
-         void* workspace, size_t ws_bytes, void* stream, const double* tensor_scales = nullptr) {
+         void* workspace, size_t ws_bytes, void* stream, const double* tensor_scales = nullptr, int shard = 0,
+         int nshards = 1) {
   validate(t, nt);
+  if (nshards < 1 || shard < 0 || shard >= nshards) throw Error(-FKS_EINVAL, "bad shard");
   if (k < 0 || (k > 0 && (!seeds || !values))) throw Error(-FKS_EINVAL, "bad seed/value arrays");
   if (value_kind != FKS_VALUE_SCALAR && value_kind != FKS_VALUE_TENSOR)
     throw Error(-FKS_EINVAL, "bad value_kind");
@@ -169,8 +223,10 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
   Layout L = make_layout(t, nt);
   if (!L.irregular.empty())
     throw Error(-FKS_ENOTSUP, "irregular tensor layout not supported by the MI355X fast path: " + L.irregular);
+  const BlockRange br = shard_blocks(L.stream_len, shard, nshards);
+  clip_segments(L, br);
   if (k == 0 || nsegs_total(L) == 0) return;
-  Plan P = make_plan(L.stream_len);
+  Plan P = make_plan(br);
   const WsLayout W = ws_layout(P.nchunks, nsegs_total(L), k);
   if (!workspace || ws_bytes < W.total)
     throw Error(-FKS_EINVAL, "workspace too small: need " + std::to_string(W.total) + " bytes, got " +
@@ -207,7 +263,7 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
     ja.states = reinterpret_cast<uint32_t*>(ws + W.off_states);
     ja.nchunks = P.nchunks;
     ja.chunks_per_wg = chunks_per_wg;
-    int rc = launch_jump(ja, nb, stream);
+    int rc = timed(1, stream, [&] { return launch_jump(ja, nb, stream); });
     if (rc) throw Error(-FKS_EHIP, std::string("fks_jump_kernel launch: ") + hipGetErrorString((hipError_t)rc));
     for (int d = 0; d < 3; d++) {
       if (L.segs[d].empty()) continue;
@@ -220,7 +276,7 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
       aa.nchunks = P.nchunks;
       aa.nseeds = nb;
       aa.mode = mode;
-      rc = launch_apply(d, aa, stream);
+      rc = timed(0, stream, [&] { return launch_apply(d, aa, stream); });
       if (rc) throw Error(rc < 0 ? rc : -FKS_EHIP, std::string("fks_apply_kernel launch: ") +
                                                          (rc > 0 ? hipGetErrorString((hipError_t)rc) : "unsupported"));
     }
@@ -257,13 +313,60 @@ int fks_workspace_size(const fks_tensor* t, int32_t nt, int32_t k, size_t* bytes
     validate(t, nt);
     if (!bytes || k < 0) throw Error(-FKS_EINVAL, "bad arguments");
     Layout L = make_layout(t, nt);
-    *bytes = ws_layout(plan_nchunks(L.stream_len), nsegs_total(L), std::max(k, 1)).total;
+    const BlockRange br = shard_blocks(L.stream_len, 0, 1);
+    *bytes = ws_layout(plan_nchunks(br.hi - br.lo), nsegs_total(L), std::max(k, 1)).total;
   });
 }
 
 int fks_directional_step(const fks_tensor* t, int32_t nt, const uint64_t* seeds, const double* values, int32_t k,
                          int32_t value_kind, void* workspace, size_t ws_bytes, void* stream) {
   return guarded([&] { run(t, nt, seeds, values, k, value_kind, kModeUpdate, workspace, ws_bytes, stream); });
+}
+
+int fks_directional_step_shard(const fks_tensor* t, int32_t nt, const uint64_t* seeds, const double* values,
+                               int32_t k, int32_t value_kind, int32_t shard, int32_t nshards, void* workspace,
+                               size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    run(t, nt, seeds, values, k, value_kind, kModeUpdate, workspace, ws_bytes, stream, nullptr, shard, nshards);
+  });
+}
+
+int fks_stream_length(const fks_tensor* t, int32_t nt, int64_t* words) {
+  return guarded([&] {
+    validate(t, nt);
+    if (!words) throw Error(-FKS_EINVAL, "null output");
+    *words = make_layout(t, nt).stream_len;
+  });
+}
+
+int fks_profile_begin(void) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_prof.on = true;
+  return 0;
+}
+
+int fks_profile_end(double* apply_ms, int64_t* n_apply, double* jump_ms, int64_t* n_jump) {
+  return guarded([&] {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    double tot[2] = {0.0, 0.0};
+    for (int w = 0; w < 2; w++) {
+      for (auto& e : g_prof.ev[w]) {
+        hipEventSynchronize(e.second);
+        float ms = 0.0f;
+        hipEventElapsedTime(&ms, e.first, e.second);
+        tot[w] += ms;
+        hipEventDestroy(e.first);
+        hipEventDestroy(e.second);
+      }
+    }
+    if (apply_ms) *apply_ms = tot[0];
+    if (jump_ms) *jump_ms = tot[1];
+    if (n_apply) *n_apply = (int64_t)g_prof.ev[0].size();
+    if (n_jump) *n_jump = (int64_t)g_prof.ev[1].size();
+    g_prof.ev[0].clear();
+    g_prof.ev[1].clear();
+    g_prof.on = false;
+  });
 }
 
 int fks_perturb(const fks_tensor* t, int32_t nt, uint64_t seed, const double* scales, void* workspace,

@@ -110,8 +110,11 @@ def _seed_u64(s) -> int:
 
 
 def directional_step(specs: Sequence[ParamSpec], seeds: Sequence[int], values: Sequence[float],
-                     value_is_tensor: bool = False) -> None:
-    """For each (seed, value) in order: p <- p - lr*(value*z + wd*p) over ``specs``."""
+                     value_is_tensor: bool = False, shard: int = 0, nshards: int = 1) -> None:
+    """For each (seed, value) in order: p <- p - lr*(value*z + wd*p) over ``specs``.
+
+    ``shard``/``nshards``: only the shard-th of nshards equal runs of MT19937 blocks of
+    the parameter stream is updated (element sharding across ranks; bit-identical)."""
     if len(seeds) != len(values):
         raise ValueError("seeds and values differ in length")
     if not specs or not len(seeds):
@@ -124,9 +127,10 @@ def directional_step(specs: Sequence[ParamSpec], seeds: Sequence[int], values: S
     v = np.ascontiguousarray([float(x) for x in values], dtype=np.float64)
     with torch.cuda.device(b.device):
         ws, nbytes = b.workspace(len(s))
-        N.check(L.fks_directional_step(ctypes.addressof(b.arr), b.n, s.ctypes.data, v.ctypes.data, len(s),
-                                       N.VALUE_TENSOR if value_is_tensor else N.VALUE_SCALAR,
-                                       ws.data_ptr(), nbytes, _stream_handle(b.device)))
+        N.check(L.fks_directional_step_shard(ctypes.addressof(b.arr), b.n, s.ctypes.data, v.ctypes.data, len(s),
+                                             N.VALUE_TENSOR if value_is_tensor else N.VALUE_SCALAR,
+                                             int(shard), int(nshards), ws.data_ptr(), nbytes,
+                                             _stream_handle(b.device)))
         b.finish()
 
 
@@ -166,6 +170,29 @@ def normal_(tensors: Sequence[torch.Tensor], seed: int, frozen: Optional[Sequenc
         N.check(L.fks_normal(ctypes.addressof(b.arr), b.n, _seed_u64(seed), ws.data_ptr(), nbytes,
                              _stream_handle(b.device)))
         b.finish()
+
+
+def stream_length(tensors: Sequence[torch.Tensor]) -> int:
+    """32-bit MT19937 words the tensors consume per seed (their z-stream length)."""
+    b = _Batch([ParamSpec(t) for t in tensors])
+    out = ctypes.c_int64(0)
+    N.check(N.load().fks_stream_length(ctypes.addressof(b.arr), b.n, ctypes.byref(out)))
+    return int(out.value)
+
+
+class profile:
+    """Context manager: device time of every codec kernel launched inside (HIP events)."""
+
+    def __enter__(self):
+        N.check(N.load().fks_profile_begin())
+        return self
+
+    def __exit__(self, *exc):
+        a, j = ctypes.c_double(0), ctypes.c_double(0)
+        na, nj = ctypes.c_int64(0), ctypes.c_int64(0)
+        N.check(N.load().fks_profile_end(ctypes.byref(a), ctypes.byref(na), ctypes.byref(j), ctypes.byref(nj)))
+        self.apply_ms, self.n_apply, self.jump_ms, self.n_jump = a.value, na.value, j.value, nj.value
+        return False
 
 
 def resolve_groups(param_groups: List[dict], lr=None, weight_decay=None) -> List[ParamSpec]:

@@ -88,6 +88,24 @@ int fks_workspace_size(const fks_tensor* t, int32_t nt, int32_t k, size_t* bytes
 int fks_directional_step(const fks_tensor* t, int32_t nt, const uint64_t* seeds, const double* values,
                          int32_t k, int32_t value_kind, void* workspace, size_t ws_bytes, void* stream);
 
+/* fks_directional_step restricted to shard `shard` of `nshards` equal runs of whole
+ * 624-word MT19937 blocks of the parameter stream: elements outside the shard are not
+ * touched.  The union over shards is bit-identical to fks_directional_step (every
+ * element still sees every seed in order); used for element-sharded multi-GPU
+ * reconstruction (one rank per shard, no collective). */
+int fks_directional_step_shard(const fks_tensor* t, int32_t nt, const uint64_t* seeds, const double* values,
+                               int32_t k, int32_t value_kind, int32_t shard, int32_t nshards, void* workspace,
+                               size_t ws_bytes, void* stream);
+
+/* Number of 32-bit generator words the tensor list consumes per seed (its stream length). */
+int fks_stream_length(const fks_tensor* t, int32_t nt, int64_t* words);
+
+/* Instrumentation (bench.py): while enabled, every kernel launch is bracketed by HIP
+ * events on the caller's stream; fks_profile_end synchronises them and returns the
+ * summed device time of the apply and jump kernels and their launch counts. */
+int fks_profile_begin(void);
+int fks_profile_end(double* apply_ms, int64_t* n_apply, double* jump_ms, int64_t* n_jump);
+
 /* torch.manual_seed(seed); for every tensor i in order: p = p + scales[i]*z, where
  * scales[i] = scaling_factor*eps of the tensor's group, computed in double by the
  * caller (optimizer.py:167,173).  Tensors with requires_grad=False draw nothing in

@@ -1,0 +1,44 @@
+"""Summarise rocprofv3 output for the apply kernel into profiles/ (per-launch, per-param)."""
+import csv, collections, json, sys, os
+
+def per_kernel(path, name_sub):
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(set)
+    grid = {}
+    for r in csv.DictReader(open(path)):
+        if name_sub not in r["Kernel_Name"]:
+            continue
+        kn = "apply<full>" if "true" in r["Kernel_Name"] else ("apply<partial>" if "false" in r["Kernel_Name"] else r["Kernel_Name"][:40])
+        agg[kn][r["Counter_Name"]] += float(r["Counter_Value"])
+        disp[kn].add(r["Dispatch_Id"])
+    return {k: {c: v / len(disp[k]) for c, v in d.items()} | {"dispatches": len(disp[k])} for k, d in agg.items()}
+
+def main(tag, params, seeds_full):
+    base = f"gpurun_out/prof_{tag}"
+    f = per_kernel(f"{base}/pmc_fetch/bench_counter_collection.csv", "fks_apply")
+    w = per_kernel(f"{base}/pmc_write/bench_counter_collection.csv", "fks_apply")
+    sq = per_kernel(f"{base}/pmc_sq/bench_counter_collection.csv", "fks_apply")
+    full = "apply<full>"
+    fetch_kb = f[full]["FETCH_SIZE"]; write_kb = w[full]["WRITE_SIZE"]
+    # gfx950: FETCH_SIZE reports 1/2 of a wide streaming read's bytes (MI355X_MICROARCH.md §HBM)
+    hbm = (2 * fetch_kb + write_kb) * 1024
+    valu = sq[full]["SQ_INSTS_VALU"] * 64
+    units = params * seeds_full
+    out = {
+        "source": f"rocprofv3 --pmc on bench.py --params {params} --k 512 (gpurun_out/prof_{tag})",
+        "apply_full_per_launch": {"FETCH_SIZE_kB": fetch_kb, "WRITE_SIZE_kB": write_kb, **sq[full]},
+        "hbm_bytes_per_launch_corrected": hbm,
+        "hbm_bytes_per_param_per_launch": hbm / params,
+        "algorithmic_bytes_per_param_per_launch": 4.0,
+        "valu_lane_ops_per_seed_param": valu / units,
+        "lds_bank_conflict_frac": sq[full]["SQ_LDS_BANK_CONFLICT"] / sq[full]["SQ_LDS_IDX_ACTIVE"],
+        "wait_any_frac": sq[full]["SQ_WAIT_ANY"] / sq[full]["SQ_WAVE_CYCLES"],
+    }
+    print(json.dumps(out, indent=1))
+    return out
+
+if __name__ == "__main__":
+    tag = sys.argv[1]; params = int(sys.argv[2]); seeds = int(sys.argv[3])
+    o = main(tag, params, seeds)
+    with open(f"profiles/pmc_apply_{tag}.json", "w") as fh:
+        json.dump(o, fh, indent=1)
