@@ -29,50 +29,108 @@ thread_local std::string g_last_error;
 struct Layout {
   int64_t stream_len = 0;
   std::vector<int64_t> offset;  // per tensor
-  std::vector<DevSeg> segs[3];  // regular segments per dtype (non-frozen tensors only)
-  std::string irregular;        // description of the first unsupported tensor, if any
+  std::vector<DevSeg> segs[3];  // fast-path segments per dtype (non-frozen tensors only)
+  std::vector<DevRun> runs;     // irregular 16-block runs (all dtypes), sorted by start
+  std::vector<DevTiny> tiny;    // single elements of numel < 16 tensors, sorted by word
+  // host-only: the tensor index of every segment / run / element (fks_shard_census)
+  std::vector<int> seg_tensor[3], run_tensor, tiny_tensor;
 };
 
+inline size_t elem_size(int dtype) { return dtype == FKS_F32 ? 4 : 2; }
+
+// The fast kernel takes a tensor whose 16-blocks sit on 16-aligned stream words (so
+// none straddles an MT block), with no tail recompute, f32/bf16, 2-element aligned
+// (it moves adjacent element pairs); everything else goes to the irregular kernel.
 Layout make_layout(const fks_tensor* t, int nt) {
   Layout L;
   L.offset.resize((size_t)nt);
-  bool cached = false;
+  bool cached = false;   // CPUGeneratorImpl::next_double_normal_sample
+  int64_t cached_pair = 0;
   int64_t pos = 0;
   for (int i = 0; i < nt; i++) {
     const fks_tensor& x = t[i];
     L.offset[(size_t)i] = pos;
     const int64_t n = x.numel;
-    const bool frozen = (x.flags & FKS_FROZEN) != 0;
+    const bool live = (x.flags & FKS_FROZEN) == 0;
+    const uint64_t ptr = (uint64_t)(uintptr_t)x.data;
+    const size_t es = elem_size(x.dtype);
     if (n >= 16) {
-      const bool regular = (n % 16 == 0) && (pos % 16 == 0);
-      if (!frozen) {
-        if (regular) {
-          DevSeg s{};
-          s.start = pos;
-          s.numel = n;
-          s.ptr = (uint64_t)(uintptr_t)x.data;
-          s.lr = x.lr;
-          s.wd = x.wd;
-          s.flags = x.flags;
-          s.dtype = x.dtype;
-          L.segs[x.dtype].push_back(s);
-        } else if (L.irregular.empty()) {
-          L.irregular = "tensor " + std::to_string(i) + " (numel " + std::to_string(n) + ", stream offset " +
-                        std::to_string(pos) + ") is not on the 16-aligned fast path";
+      const bool fast = n % 16 == 0 && pos % 16 == 0 && x.dtype != FKS_F16 && ptr % (2 * es) == 0;
+      if (live && fast) {
+        DevSeg s{};
+        s.start = pos;
+        s.numel = n;
+        s.ptr = ptr;
+        s.lr = x.lr;
+        s.wd = x.wd;
+        s.flags = x.flags;
+        s.dtype = x.dtype;
+        L.segs[x.dtype].push_back(s);
+        L.seg_tensor[x.dtype].push_back(i);
+      } else if (live) {
+        // words [pos, pos + 16F) hold F = n / 16 whole 16-blocks; if n % 16 != 0 the last
+        // 16 elements are redrawn from 16 fresh words [pos + n, pos + n + 16) and the head
+        // run must not write them (DistributionTemplates.h:118-124 / :221-228)
+        const int64_t F = n / 16;
+        DevRun r{};
+        r.start = pos;
+        r.numel = 16 * F;
+        r.ptr = ptr;
+        r.limit = n % 16 ? n - 16 : n;
+        r.lr = x.lr;
+        r.wd = x.wd;
+        r.flags = x.flags;
+        r.dtype = x.dtype;
+        L.runs.push_back(r);
+        L.run_tensor.push_back(i);
+        if (n % 16) {
+          DevRun tl = r;
+          tl.start = pos + n;
+          tl.numel = 16;
+          tl.ptr = ptr + (uint64_t)(n - 16) * es;
+          tl.limit = 16;
+          L.runs.push_back(tl);
+          L.run_tensor.push_back(i);
         }
       }
       pos += n + (n % 16 ? 16 : 0);
     } else if (n > 0) {
-      if (!frozen && L.irregular.empty())
-        L.irregular = "tensor " + std::to_string(i) + " has numel " + std::to_string(n) +
-                      " < 16 (torch's serial normal_distribution<double> path)";
       for (int64_t e = 0; e < n; e++) {
-        if (cached) cached = false;
-        else { pos += 4; cached = true; }
+        DevTiny d{};
+        if (cached) {
+          cached = false;
+          d.word = cached_pair;
+          d.flags = kTinySin;
+        } else {
+          cached = true;
+          cached_pair = d.word = pos;
+          pos += 4;
+        }
+        if (!live) continue;
+        d.ptr = ptr + (uint64_t)e * es;
+        d.lr = x.lr;
+        d.wd = x.wd;
+        d.flags |= x.flags & FKS_HAS_WD;
+        d.dtype = x.dtype;
+        L.tiny.push_back(d);
+        L.tiny_tensor.push_back(i);
       }
     }
   }
   L.stream_len = pos;
+  // runs are disjoint and already in stream order; single elements sorted by the
+  // block holding their last word, the order the kernel walks them in
+  std::vector<size_t> order(L.tiny.size());
+  for (size_t j = 0; j < order.size(); j++) order[j] = j;
+  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return L.tiny[a].word < L.tiny[b].word; });
+  std::vector<DevTiny> tiny(order.size());
+  std::vector<int> tiny_tensor(order.size());
+  for (size_t j = 0; j < order.size(); j++) {
+    tiny[j] = L.tiny[order[j]];
+    tiny_tensor[j] = L.tiny_tensor[order[j]];
+  }
+  L.tiny.swap(tiny);
+  L.tiny_tensor.swap(tiny_tensor);
   return L;
 }
 
@@ -83,9 +141,7 @@ void validate(const fks_tensor* t, int nt) {
     if (x.numel < 0) throw Error(-FKS_EINVAL, "tensor " + std::to_string(i) + ": negative numel");
     if (x.dtype != FKS_F32 && x.dtype != FKS_BF16 && x.dtype != FKS_F16)
       throw Error(-FKS_EINVAL, "tensor " + std::to_string(i) + ": unsupported dtype code " + std::to_string(x.dtype));
-    if (x.dtype == FKS_F16)
-      throw Error(-FKS_ENOTSUP, "tensor " + std::to_string(i) + ": float16 parameters are not implemented on the MI355X path yet");
-    const size_t es = x.dtype == FKS_F32 ? 4 : 2;
+    const size_t es = elem_size(x.dtype);
     if (x.numel > 0 && (!x.data || ((uintptr_t)x.data % es) != 0))
       throw Error(-FKS_EINVAL, "tensor " + std::to_string(i) + ": null or misaligned data pointer");
     if (x.flags & ~(FKS_HAS_WD | FKS_FROZEN)) throw Error(-FKS_EINVAL, "tensor " + std::to_string(i) + ": unknown flags");
@@ -111,73 +167,211 @@ int plan_nchunks(int64_t nblocks) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(nblocks, target));
 }
 
-Plan make_plan(BlockRange r) {
+Plan plan_from_blocks(std::vector<int64_t> chunk_block) {
   Plan P;
-  const int64_t nblocks = std::max<int64_t>(1, r.hi - r.lo);
-  P.nchunks = plan_nchunks(nblocks);
-  P.chunk_block.resize((size_t)P.nchunks + 1);
-  for (int c = 0; c <= P.nchunks; c++)
-    P.chunk_block[(size_t)c] = r.lo + (int64_t)((__int128)nblocks * c / P.nchunks);
+  P.nchunks = (int)chunk_block.size() - 1;
+  P.chunk_block = std::move(chunk_block);
   std::vector<int64_t> starts(P.chunk_block.begin(), P.chunk_block.end() - 1);
   jump_polys_for_blocks(starts, P.polys);
   return P;
 }
 
-// keep only the part of every segment inside the block range (16-aligned cuts)
+Plan make_plan(BlockRange r) {
+  const int64_t nblocks = std::max<int64_t>(1, r.hi - r.lo);
+  const int nchunks = plan_nchunks(nblocks);
+  std::vector<int64_t> cb((size_t)nchunks + 1);
+  for (int c = 0; c <= nchunks; c++) cb[(size_t)c] = r.lo + (int64_t)((__int128)nblocks * c / nchunks);
+  return plan_from_blocks(std::move(cb));
+}
+
+// MT block holding stream word w
+inline int64_t block_of(int64_t w) { return w / kMtN; }
+
+// keep only the work whose owner block lies in the range: fast segments are cut at
+// block boundaries (16-aligned), a run keeps the 16-blocks whose last word is inside,
+// a single element stays where its draw pair ends
 void clip_segments(Layout& L, BlockRange r) {
   const int64_t lo = r.lo * kMtN, hi = r.hi * kMtN;
   for (int d = 0; d < 3; d++) {
     std::vector<DevSeg> out;
-    for (const DevSeg& s : L.segs[d]) {
+    std::vector<int> out_t;
+    for (size_t j = 0; j < L.segs[d].size(); j++) {
+      const DevSeg& s = L.segs[d][j];
       const int64_t a = std::max(s.start, lo), b = std::min(s.start + s.numel, hi);
       if (a >= b) continue;
       DevSeg c = s;
-      const size_t es = s.dtype == FKS_F32 ? 4 : 2;
-      c.ptr = s.ptr + (uint64_t)(a - s.start) * es;
+      c.ptr = s.ptr + (uint64_t)(a - s.start) * elem_size(s.dtype);
       c.start = a;
       c.numel = b - a;
       out.push_back(c);
+      out_t.push_back(L.seg_tensor[d][j]);
     }
     L.segs[d].swap(out);
+    L.seg_tensor[d].swap(out_t);
   }
+  std::vector<DevRun> runs;
+  std::vector<int> runs_t;
+  for (size_t j = 0; j < L.runs.size(); j++) {
+    const DevRun& R = L.runs[j];
+    const int64_t nb = R.numel / 16;
+    // 16-block i ends at word R.start + 16 i + 15
+    auto first_at_or_after = [&](int64_t w) {
+      const int64_t d = w - (R.start + 15);
+      return std::min(nb, std::max<int64_t>(0, (d + 15) / 16 * (d > 0)));
+    };
+    const int64_t i0 = first_at_or_after(lo), i1 = first_at_or_after(hi);
+    if (i0 >= i1) continue;
+    DevRun c = R;
+    c.start = R.start + 16 * i0;
+    c.numel = 16 * (i1 - i0);
+    c.ptr = R.ptr + (uint64_t)(16 * i0) * elem_size(R.dtype);
+    c.limit = R.limit - 16 * i0;
+    runs.push_back(c);
+    runs_t.push_back(L.run_tensor[j]);
+  }
+  L.runs.swap(runs);
+  L.run_tensor.swap(runs_t);
+  std::vector<DevTiny> tiny;
+  std::vector<int> tiny_t;
+  for (size_t j = 0; j < L.tiny.size(); j++) {
+    const DevTiny& T = L.tiny[j];
+    if (T.word + 3 >= lo && T.word + 3 < hi) {
+      tiny.push_back(T);
+      tiny_t.push_back(L.tiny_tensor[j]);
+    }
+  }
+  L.tiny.swap(tiny);
+  L.tiny_tensor.swap(tiny_t);
+}
+
+// Chunks of the irregular kernel: the MT blocks that own irregular work, split into at
+// most plan_nchunks() groups of about equal work; a chunk twists through the blocks
+// between its first and last owner block.
+struct IrrChunks {
+  std::vector<int64_t> lo, hi;  // chunk c twists blocks [lo[c], hi[c])
+};
+std::vector<std::pair<int64_t, int64_t>> irregular_owner_intervals(const Layout& L) {
+  std::vector<std::pair<int64_t, int64_t>> iv;  // owner block intervals [a, b)
+  for (const DevRun& R : L.runs) iv.emplace_back(block_of(R.start + 15), block_of(R.start + R.numel - 1) + 1);
+  for (const DevTiny& T : L.tiny) iv.emplace_back(block_of(T.word + 3), block_of(T.word + 3) + 1);
+  std::sort(iv.begin(), iv.end());
+  std::vector<std::pair<int64_t, int64_t>> merged;
+  for (auto& x : iv) {
+    if (!merged.empty() && x.first <= merged.back().second) merged.back().second = std::max(merged.back().second, x.second);
+    else merged.push_back(x);
+  }
+  return merged;
+}
+
+int64_t irregular_covered_blocks(const Layout& L) {
+  int64_t covered = 0;
+  for (auto& x : irregular_owner_intervals(L)) covered += x.second - x.first;
+  return covered;
+}
+
+IrrChunks irregular_chunks(const Layout& L) {
+  const auto merged = irregular_owner_intervals(L);
+  if (merged.empty()) return IrrChunks{};
+  int64_t covered = 0;
+  for (auto& x : merged) covered += x.second - x.first;
+  const int cap = plan_nchunks(covered);
+  const int64_t q = (covered + cap - 1) / cap;  // owner blocks per chunk
+  IrrChunks out;
+  int64_t in_chunk = 0, chunk_lo = -1, last_hi = -1;
+  auto close = [&] {
+    out.lo.push_back(chunk_lo);
+    out.hi.push_back(last_hi);
+    chunk_lo = -1;
+    in_chunk = 0;
+  };
+  for (auto& x : merged) {
+    int64_t a = x.first;
+    while (a < x.second) {
+      if (chunk_lo < 0) chunk_lo = a;
+      const int64_t take = std::min(x.second - a, q - in_chunk);
+      a += take;
+      in_chunk += take;
+      last_hi = a;
+      if (in_chunk == q) close();
+    }
+  }
+  if (chunk_lo >= 0) close();
+  return out;
 }
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Workspace: [header uploaded once per call | generator windows].  Both plans (fast
+// and irregular) share the window area: they run one after the other on the stream.
+struct WsSizes {
+  int reg_chunks = 0, irr_chunks = 0, nsegs = 0, nruns = 0, ntiny = 0, k = 0;
+};
+
 struct WsLayout {
-  size_t header = 0;      // bytes of the uploaded header (polys, chunk_block, segs, seeds, g)
-  size_t off_polys = 0, off_cb = 0, off_segs = 0, off_seeds = 0, off_g = 0, off_states = 0;
+  size_t header = 0;  // bytes of the uploaded header
+  size_t off_polys = 0, off_cb = 0, off_ipolys = 0, off_ilo = 0, off_ihi = 0, off_segs = 0, off_runs = 0,
+         off_tiny = 0, off_seeds = 0, off_g = 0, off_states = 0;
   size_t total = 0;
 };
 
-WsLayout ws_layout(int nchunks, int nsegs_total, int k) {
+WsLayout ws_layout(const WsSizes& z) {
   WsLayout w;
   size_t o = 0;
-  w.off_polys = o; o = align_up(o + sizeof(uint64_t) * 312 * (size_t)nchunks, 256);
-  w.off_cb = o;    o = align_up(o + sizeof(int64_t) * ((size_t)nchunks + 1), 256);
-  w.off_segs = o;  o = align_up(o + sizeof(DevSeg) * (size_t)std::max(nsegs_total, 1), 256);
-  w.off_seeds = o; o = align_up(o + sizeof(uint64_t) * (size_t)std::max(k, 1), 256);
-  w.off_g = o;     o = align_up(o + sizeof(float) * 3 * (size_t)std::max(k, 1), 256);
+  auto put = [&](size_t& off, size_t bytes) { off = o; o = align_up(o + std::max<size_t>(bytes, 1), 256); };
+  const size_t k = (size_t)std::max(z.k, 1);
+  put(w.off_polys, sizeof(uint64_t) * 312 * (size_t)z.reg_chunks);
+  put(w.off_cb, sizeof(int64_t) * ((size_t)z.reg_chunks + 1));
+  put(w.off_ipolys, sizeof(uint64_t) * 312 * (size_t)z.irr_chunks);
+  put(w.off_ilo, sizeof(int64_t) * (size_t)z.irr_chunks);
+  put(w.off_ihi, sizeof(int64_t) * (size_t)z.irr_chunks);
+  put(w.off_segs, sizeof(DevSeg) * (size_t)z.nsegs);
+  put(w.off_runs, sizeof(DevRun) * (size_t)z.nruns);
+  put(w.off_tiny, sizeof(DevTiny) * (size_t)z.ntiny);
+  put(w.off_seeds, sizeof(uint64_t) * k);
+  put(w.off_g, sizeof(float) * 3 * k);
   w.header = o;
-  w.off_states = o;
-  o = align_up(o + sizeof(uint32_t) * kMtN * (size_t)kMaxSeedsPerPass * (size_t)nchunks, 256);
+  const size_t chunks = (size_t)std::max(z.reg_chunks, z.irr_chunks);
+  put(w.off_states, sizeof(uint32_t) * kMtN * (size_t)kMaxSeedsPerPass * chunks);
   w.total = o;
   return w;
 }
 
 int nsegs_total(const Layout& L) { return (int)(L.segs[0].size() + L.segs[1].size() + L.segs[2].size()); }
 
+// float -> binary16 -> float, round to nearest even (c10::Half)
+inline float round_f16(float f) {
+  uint32_t x;
+  std::memcpy(&x, &f, 4);
+  const uint32_t sign = x & 0x80000000u, ax = x & 0x7fffffffu;
+  float r;
+  if (ax >= 0x477ff000u) {
+    x = sign | 0x7f800000u;
+  } else if (ax < 0x38800000u) {  // half subnormal: quantum 2^-24
+    std::memcpy(&r, &ax, 4);
+    r = std::nearbyint(r * 16777216.0f) / 16777216.0f;
+    std::memcpy(&x, &r, 4);
+    x |= sign;
+  } else {
+    uint32_t keep = ax & ~0x1fffu;
+    const uint32_t rem = ax & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (keep & 0x2000u))) keep += 0x2000u;
+    x = sign | keep;
+  }
+  std::memcpy(&r, &x, 4);
+  return r;
+}
+
+// a 0-dim fp32 tensor g enters `g * z` as the first operand: torch casts it to the
+// parameter dtype first (zo step's g, optimizer.py:147)
 inline float round_to_dtype(double v, int dtype) {
   float f = (float)v;
   if (dtype == FKS_F32 || f != f) return f;
+  if (dtype == FKS_F16) return round_f16(f);
   uint32_t u;
   std::memcpy(&u, &f, 4);
-  if (dtype == FKS_BF16) {
-    u = (u + (((u >> 16) & 1u) + 0x7FFFu)) & 0xFFFF0000u;
-    std::memcpy(&f, &u, 4);
-    return f;
-  }
-  return f;  // f16 not reachable (rejected in validate)
+  u = (u + (((u >> 16) & 1u) + 0x7FFFu)) & 0xFFFF0000u;
+  std::memcpy(&f, &u, 4);
+  return f;
 }
 
 // Core: run `k` seeds (update / perturb / write-z) over the tensor list.
@@ -197,11 +391,11 @@ int timed(int which, void* stream, F&& launch) {
     return launch();
   }
   hipEvent_t a, b;
-  hipEventCreate(&a);
-  hipEventCreate(&b);
-  hipEventRecord(a, (hipStream_t)stream);
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  (void)hipEventRecord(a, (hipStream_t)stream);
   const int rc = launch();
-  hipEventRecord(b, (hipStream_t)stream);
+  (void)hipEventRecord(b, (hipStream_t)stream);
   g_prof.ev[which].emplace_back(a, b);
   return rc;
 }
@@ -221,13 +415,23 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
     t = tt.data();
   }
   Layout L = make_layout(t, nt);
-  if (!L.irregular.empty())
-    throw Error(-FKS_ENOTSUP, "irregular tensor layout not supported by the MI355X fast path: " + L.irregular);
   const BlockRange br = shard_blocks(L.stream_len, shard, nshards);
   clip_segments(L, br);
-  if (k == 0 || nsegs_total(L) == 0) return;
-  Plan P = make_plan(br);
-  const WsLayout W = ws_layout(P.nchunks, nsegs_total(L), k);
+  const bool have_reg = nsegs_total(L) > 0, have_irr = !L.runs.empty() || !L.tiny.empty();
+  if (k == 0 || (!have_reg && !have_irr)) return;
+  Plan P;
+  if (have_reg) P = make_plan(br);
+  const IrrChunks IC = irregular_chunks(L);
+  std::vector<uint64_t> ipolys;
+  if (have_irr) jump_polys_for_blocks(IC.lo, ipolys);
+  WsSizes z;
+  z.reg_chunks = P.nchunks;
+  z.irr_chunks = (int)IC.lo.size();
+  z.nsegs = nsegs_total(L);
+  z.nruns = (int)L.runs.size();
+  z.ntiny = (int)L.tiny.size();
+  z.k = k;
+  const WsLayout W = ws_layout(z);
   if (!workspace || ws_bytes < W.total)
     throw Error(-FKS_EINVAL, "workspace too small: need " + std::to_string(W.total) + " bytes, got " +
                                  std::to_string(ws_bytes));
@@ -235,16 +439,24 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
   // source is staged before hipMemcpyAsync returns, so the buffer is reusable)
   thread_local std::vector<uint8_t> host;
   host.assign(W.header, 0);
-  std::memcpy(host.data() + W.off_polys, P.polys.data(), sizeof(uint64_t) * P.polys.size());
-  std::memcpy(host.data() + W.off_cb, P.chunk_block.data(), sizeof(int64_t) * P.chunk_block.size());
+  auto put = [&](size_t off, const void* src, size_t bytes) {
+    if (bytes) std::memcpy(host.data() + off, src, bytes);
+  };
+  put(W.off_polys, P.polys.data(), sizeof(uint64_t) * P.polys.size());
+  put(W.off_cb, P.chunk_block.data(), sizeof(int64_t) * P.chunk_block.size());
+  put(W.off_ipolys, ipolys.data(), sizeof(uint64_t) * ipolys.size());
+  put(W.off_ilo, IC.lo.data(), sizeof(int64_t) * IC.lo.size());
+  put(W.off_ihi, IC.hi.data(), sizeof(int64_t) * IC.hi.size());
   size_t so = W.off_segs;
   size_t seg_off[3];
   for (int d = 0; d < 3; d++) {
     seg_off[d] = so;
-    if (!L.segs[d].empty()) std::memcpy(host.data() + so, L.segs[d].data(), sizeof(DevSeg) * L.segs[d].size());
+    put(so, L.segs[d].data(), sizeof(DevSeg) * L.segs[d].size());
     so += sizeof(DevSeg) * L.segs[d].size();
   }
-  std::memcpy(host.data() + W.off_seeds, seeds, sizeof(uint64_t) * (size_t)k);
+  put(W.off_runs, L.runs.data(), sizeof(DevRun) * L.runs.size());
+  put(W.off_tiny, L.tiny.data(), sizeof(DevTiny) * L.tiny.size());
+  put(W.off_seeds, seeds, sizeof(uint64_t) * (size_t)k);
   float* gh = reinterpret_cast<float*>(host.data() + W.off_g);
   for (int d = 0; d < 3; d++)
     for (int s = 0; s < k; s++)
@@ -253,32 +465,61 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
   hipError_t e = hipMemcpyAsync(ws, host.data(), W.header, hipMemcpyHostToDevice, (hipStream_t)stream);
   if (e != hipSuccess) throw Error(-FKS_EHIP, std::string("hipMemcpyAsync: ") + hipGetErrorString(e));
 
-  const int chunks_per_wg = std::max(1, std::min(32, P.nchunks));  // 2 jumps per wave (16 waves)
+  auto check = [](int rc, const char* what) {
+    if (rc) throw Error(rc < 0 ? rc : -FKS_EHIP, std::string(what) + " launch: " +
+                                                   (rc > 0 ? hipGetErrorString((hipError_t)rc) : "unsupported"));
+  };
+  uint32_t* states = reinterpret_cast<uint32_t*>(ws + W.off_states);
+  const uint64_t* dseeds = reinterpret_cast<const uint64_t*>(ws + W.off_seeds);
+  const float* dg = reinterpret_cast<const float*>(ws + W.off_g);
   for (int s0 = 0; s0 < k; s0 += kMaxSeedsPerPass) {
     const int nb = std::min(kMaxSeedsPerPass, k - s0);
-    JumpArgs ja{};
-    ja.seeds = reinterpret_cast<const uint64_t*>(ws + W.off_seeds) + s0;
-    ja.polys = reinterpret_cast<const uint64_t*>(ws + W.off_polys);
-    ja.chunk_block = reinterpret_cast<const int64_t*>(ws + W.off_cb);
-    ja.states = reinterpret_cast<uint32_t*>(ws + W.off_states);
-    ja.nchunks = P.nchunks;
-    ja.chunks_per_wg = chunks_per_wg;
-    int rc = timed(1, stream, [&] { return launch_jump(ja, nb, stream); });
-    if (rc) throw Error(-FKS_EHIP, std::string("fks_jump_kernel launch: ") + hipGetErrorString((hipError_t)rc));
-    for (int d = 0; d < 3; d++) {
-      if (L.segs[d].empty()) continue;
-      ApplyArgs aa{};
-      aa.states = ja.states;
-      aa.g = reinterpret_cast<const float*>(ws + W.off_g) + (size_t)d * k + s0;
-      aa.segs = reinterpret_cast<const DevSeg*>(ws + seg_off[d]);
-      aa.chunk_block = ja.chunk_block;
-      aa.nsegs = (int)L.segs[d].size();
-      aa.nchunks = P.nchunks;
-      aa.nseeds = nb;
-      aa.mode = mode;
-      rc = timed(0, stream, [&] { return launch_apply(d, aa, stream); });
-      if (rc) throw Error(rc < 0 ? rc : -FKS_EHIP, std::string("fks_apply_kernel launch: ") +
-                                                         (rc > 0 ? hipGetErrorString((hipError_t)rc) : "unsupported"));
+    if (have_reg) {
+      JumpArgs ja{};
+      ja.seeds = dseeds + s0;
+      ja.polys = reinterpret_cast<const uint64_t*>(ws + W.off_polys);
+      ja.chunk_block = reinterpret_cast<const int64_t*>(ws + W.off_cb);
+      ja.states = states;
+      ja.nchunks = P.nchunks;
+      ja.chunks_per_wg = std::max(1, std::min(32, P.nchunks));  // 2 jumps per wave (16 waves)
+      check(timed(1, stream, [&] { return launch_jump(ja, nb, stream); }), "fks_jump_kernel");
+      for (int d = 0; d < 3; d++) {
+        if (L.segs[d].empty()) continue;
+        ApplyArgs aa{};
+        aa.states = states;
+        aa.g = dg + (size_t)d * k + s0;
+        aa.segs = reinterpret_cast<const DevSeg*>(ws + seg_off[d]);
+        aa.chunk_block = ja.chunk_block;
+        aa.nsegs = (int)L.segs[d].size();
+        aa.nchunks = P.nchunks;
+        aa.nseeds = nb;
+        aa.mode = mode;
+        check(timed(0, stream, [&] { return launch_apply(d, aa, stream); }), "fks_apply_kernel");
+      }
+    }
+    if (have_irr) {
+      JumpArgs ja{};
+      ja.seeds = dseeds + s0;
+      ja.polys = reinterpret_cast<const uint64_t*>(ws + W.off_ipolys);
+      ja.chunk_block = reinterpret_cast<const int64_t*>(ws + W.off_ilo);
+      ja.states = states;
+      ja.nchunks = z.irr_chunks;
+      ja.chunks_per_wg = std::max(1, std::min(32, z.irr_chunks));
+      check(timed(1, stream, [&] { return launch_jump(ja, nb, stream); }), "fks_jump_kernel");
+      IrrArgs ia{};
+      ia.states = states;
+      ia.g = dg + s0;
+      ia.gstride = k;
+      ia.runs = reinterpret_cast<const DevRun*>(ws + W.off_runs);
+      ia.tiny = reinterpret_cast<const DevTiny*>(ws + W.off_tiny);
+      ia.chunk_lo = ja.chunk_block;
+      ia.chunk_hi = reinterpret_cast<const int64_t*>(ws + W.off_ihi);
+      ia.nruns = z.nruns;
+      ia.ntiny = z.ntiny;
+      ia.nchunks = z.irr_chunks;
+      ia.nseeds = nb;
+      ia.mode = mode;
+      check(timed(0, stream, [&] { return launch_irregular(ia, stream); }), "fks_irregular_kernel");
     }
   }
 }
@@ -312,9 +553,17 @@ int fks_workspace_size(const fks_tensor* t, int32_t nt, int32_t k, size_t* bytes
   return guarded([&] {
     validate(t, nt);
     if (!bytes || k < 0) throw Error(-FKS_EINVAL, "bad arguments");
-    Layout L = make_layout(t, nt);
-    const BlockRange br = shard_blocks(L.stream_len, 0, 1);
-    *bytes = ws_layout(plan_nchunks(br.hi - br.lo), nsegs_total(L), std::max(k, 1)).total;
+    const Layout L = make_layout(t, nt);
+    // upper bounds over every shard count: a shard never needs more chunks, segments,
+    // runs or single elements than the whole stream
+    WsSizes z;
+    if (nsegs_total(L)) z.reg_chunks = plan_nchunks(shard_blocks(L.stream_len, 0, 1).hi);
+    if (!L.runs.empty() || !L.tiny.empty()) z.irr_chunks = plan_nchunks(irregular_covered_blocks(L));
+    z.nsegs = nsegs_total(L);
+    z.nruns = (int)L.runs.size();
+    z.ntiny = (int)L.tiny.size();
+    z.k = std::max(k, 1);
+    *bytes = ws_layout(z).total;
   });
 }
 
@@ -339,6 +588,28 @@ int fks_stream_length(const fks_tensor* t, int32_t nt, int64_t* words) {
   });
 }
 
+int fks_shard_census(const fks_tensor* t, int32_t nt, int32_t shard, int32_t nshards, int64_t* word_range,
+                     int64_t* written) {
+  return guarded([&] {
+    validate(t, nt);
+    if (nshards < 1 || shard < 0 || shard >= nshards) throw Error(-FKS_EINVAL, "bad shard");
+    Layout L = make_layout(t, nt);
+    const BlockRange br = shard_blocks(L.stream_len, shard, nshards);
+    clip_segments(L, br);
+    if (word_range) {
+      word_range[0] = br.lo * kMtN;
+      word_range[1] = br.hi * kMtN;
+    }
+    if (!written) return;
+    for (int i = 0; i < nt; i++) written[i] = 0;
+    for (int d = 0; d < 3; d++)
+      for (size_t j = 0; j < L.segs[d].size(); j++) written[L.seg_tensor[d][j]] += L.segs[d][j].numel;
+    for (size_t j = 0; j < L.runs.size(); j++)
+      written[L.run_tensor[j]] += std::max<int64_t>(0, std::min(L.runs[j].limit, L.runs[j].numel));
+    for (size_t j = 0; j < L.tiny.size(); j++) written[L.tiny_tensor[j]] += 1;
+  });
+}
+
 int fks_profile_begin(void) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
   g_prof.on = true;
@@ -351,12 +622,12 @@ int fks_profile_end(double* apply_ms, int64_t* n_apply, double* jump_ms, int64_t
     double tot[2] = {0.0, 0.0};
     for (int w = 0; w < 2; w++) {
       for (auto& e : g_prof.ev[w]) {
-        hipEventSynchronize(e.second);
+        (void)hipEventSynchronize(e.second);
         float ms = 0.0f;
-        hipEventElapsedTime(&ms, e.first, e.second);
+        (void)hipEventElapsedTime(&ms, e.first, e.second);
         tot[w] += ms;
-        hipEventDestroy(e.first);
-        hipEventDestroy(e.second);
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
       }
     }
     if (apply_ms) *apply_ms = tot[0];

@@ -20,6 +20,10 @@
 
 #include "fks_internal.h"
 
+#ifndef FKS_DIAG
+#define FKS_DIAG 0  // diagnostic builds only (make diag): timing variants with wrong results
+#endif
+
 namespace fks {
 namespace {
 
@@ -55,12 +59,24 @@ typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 // RNE to bf16, result kept as the f32 with the same value: ONE v_cvt_pk_bf16_f32 with
 // a zero low half (hi = bf16(x), lo = bf16(0) = 0x0000).  NaN stays NaN.
-__device__ __forceinline__ float rbf(float x) {
+__device__ __forceinline__ float rbf_cvt(float x) {
   const f32x2_t v = {0.0f, x};
   return __builtin_bit_cast(float, __builtin_convertvector(v, bf16x2_t));
 }
+__device__ __forceinline__ float rbf(float x) {
+#if FKS_DIAG == 5  // diagnostics: truncation instead of RNE (wrong values)
+  return __uint_as_float(__float_as_uint(x) & 0xffff0000u);
+#else
+  return rbf_cvt(x);
+#endif
+}
 __device__ __forceinline__ float rhf(float x) {  // RNE to f16 and back
   return static_cast<float>(static_cast<_Float16>(x));
+}
+
+// value of the adjacent lane (lane ^ 1): DPP quad_perm [1,0,3,2]
+__device__ __forceinline__ uint32_t swap_adjacent(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
 }
 
 // ------------------------------------------------------------------ fp32 Box-Muller
@@ -155,8 +171,23 @@ typedef __attribute__((address_space(1))) float gf32;
 typedef __attribute__((address_space(1))) uint16_t gu16;
 typedef __attribute__((address_space(1))) _Float16 gf16;
 
+// load_raw returns the element's bits (kept raw in the software pipeline so that the
+// load's wait lands at first use, a block later); cvt turns them into the f32 value.
+typedef __attribute__((address_space(1))) uint32_t gu32;
+
+typedef __attribute__((address_space(1))) uint64_t gu64;
+
 template <>
 struct Traits<FKS_F32> {
+  typedef uint64_t Pair;  // two adjacent elements
+  __device__ static Pair load_pair(uint64_t a) { return *reinterpret_cast<const gu64*>(a); }
+  __device__ static void store_pair(uint64_t a, Pair v) { *reinterpret_cast<gu64*>(a) = v; }
+  __device__ static uint32_t lo(Pair v) { return (uint32_t)v; }
+  __device__ static uint32_t hi(Pair v) { return (uint32_t)(v >> 32); }
+  __device__ static Pair pack(uint32_t l, uint32_t h) { return (uint64_t)l | ((uint64_t)h << 32); }
+  __device__ static uint32_t bits(float v) { return __float_as_uint(v); }
+  __device__ static uint32_t load_raw(uint64_t p, int64_t i) { return reinterpret_cast<const gu32*>(p)[i]; }
+  __device__ static float cvt(uint32_t r) { return __uint_as_float(r); }
   __device__ static float load(uint64_t p, int64_t i) { return reinterpret_cast<const gf32*>(p)[i]; }
   __device__ static void store(uint64_t p, int64_t i, float v) { reinterpret_cast<gf32*>(p)[i] = v; }
   __device__ static float rnd(float x) { return x; }
@@ -164,6 +195,15 @@ struct Traits<FKS_F32> {
 
 template <>
 struct Traits<FKS_BF16> {
+  typedef uint32_t Pair;  // two adjacent elements
+  __device__ static Pair load_pair(uint64_t a) { return *reinterpret_cast<const gu32*>(a); }
+  __device__ static void store_pair(uint64_t a, Pair v) { *reinterpret_cast<gu32*>(a) = v; }
+  __device__ static uint32_t lo(Pair v) { return v & 0xffffu; }
+  __device__ static uint32_t hi(Pair v) { return v >> 16; }
+  __device__ static Pair pack(uint32_t l, uint32_t h) { return (l & 0xffffu) | (h << 16); }
+  __device__ static uint32_t bits(float v) { return __float_as_uint(v) >> 16; }  // v is bf16-exact
+  __device__ static uint32_t load_raw(uint64_t p, int64_t i) { return reinterpret_cast<const gu16*>(p)[i]; }
+  __device__ static float cvt(uint32_t r) { return __uint_as_float(r << 16); }
   __device__ static float load(uint64_t p, int64_t i) {
     return __uint_as_float((uint32_t)reinterpret_cast<const gu16*>(p)[i] << 16);
   }
@@ -175,6 +215,15 @@ struct Traits<FKS_BF16> {
 
 template <>
 struct Traits<FKS_F16> {
+  typedef uint32_t Pair;
+  __device__ static Pair load_pair(uint64_t a) { return *reinterpret_cast<const gu32*>(a); }
+  __device__ static void store_pair(uint64_t a, Pair v) { *reinterpret_cast<gu32*>(a) = v; }
+  __device__ static uint32_t lo(Pair v) { return v & 0xffffu; }
+  __device__ static uint32_t hi(Pair v) { return v >> 16; }
+  __device__ static Pair pack(uint32_t l, uint32_t h) { return (l & 0xffffu) | (h << 16); }
+  __device__ static uint32_t bits(float v) { return __builtin_bit_cast(uint16_t, static_cast<_Float16>(v)); }
+  __device__ static uint32_t load_raw(uint64_t p, int64_t i) { return reinterpret_cast<const gu16*>(p)[i]; }
+  __device__ static float cvt(uint32_t r) { return static_cast<float>(__builtin_bit_cast(_Float16, (uint16_t)r)); }
   __device__ static float load(uint64_t p, int64_t i) { return static_cast<float>(reinterpret_cast<const gf16*>(p)[i]); }
   __device__ static void store(uint64_t p, int64_t i, float v) { reinterpret_cast<gf16*>(p)[i] = static_cast<_Float16>(v); }
   __device__ static float rnd(float x) { return rhf(x); }
@@ -299,33 +348,28 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
 // reads word i+1, which another thread writes in the same phase).  Item addresses
 // depend only on (thread, nseeds), so they are computed once per kernel and the
 // three reads use immediate offsets.
-constexpr int kR12 = (227 * kMaxSeedsPerPass + kApplyThreads - 1) / kApplyThreads;  // items / thread, phases 1-2
-constexpr int kR3 = (170 * kMaxSeedsPerPass + kApplyThreads - 1) / kApplyThreads;   // items / thread, phase 3
+// Thread mapping: tid = 16 k + g (k < kMaxSeedsPerPass seeds, g < 16); item r of a
+// phase is word lo + g + 16 r of window k, so every LDS access of a phase is ONE
+// per-thread base address plus an immediate offset (64 r + phase constant), and the
+// 16 lanes of a seed touch 16 consecutive words (conflict-free).
+constexpr int kTwLanes = 16 * kMaxSeedsPerPass;   // threads with twist work
+constexpr int kR12 = (227 + 15) / 16;              // items per thread, phases 1-2 (last one partial)
+constexpr int kR3 = (170 + 15) / 16;               // items per thread, phase 3
+static_assert(kTwLanes <= kApplyThreads, "twist lanes exceed the workgroup");
 
 struct TwistPlan {
-  int a12[kR12];   // byte offset of (window k, word i') for phases 1-2
-  int a3[kR3];     // byte offset of (window k, word i'') for phase 3 (word 454 + i'')
-  uint32_t last3;  // bit r: item r of phase 3 is word 623 (its partner is the NEW word 0)
+  int base;     // byte offset of word g of window k
+  int dummy;    // a spare-window word: sink for the writes of items past the phase end
+  int g;
+  bool on;
 };
 
-// Items are dealt round-robin; an item past the last seed lands in a window that is
-// either unused in this pass or the spare window kMaxSeedsPerPass, so every item runs
-// unconditionally (no exec-masked branches, all LDS reads of a phase in flight at once).
 __device__ __forceinline__ void twist_plan(TwistPlan& P, int tid, int st_base) {
-#pragma unroll
-  for (int r = 0; r < kR12; r++) {
-    const int it = tid + r * kApplyThreads;
-    const int k = it / 227, i = it - k * 227;
-    P.a12[r] = st_base + 4 * (min(k, kMaxSeedsPerPass) * kMtN + i);  // overflow items: spare window
-  }
-  P.last3 = 0;
-#pragma unroll
-  for (int r = 0; r < kR3; r++) {
-    const int it = tid + r * kApplyThreads;
-    const int k = it / 170, i = it - k * 170;
-    P.a3[r] = st_base + 4 * (min(k, kMaxSeedsPerPass) * kMtN + i);
-    if (i == 169) P.last3 |= 1u << r;
-  }
+  const int k = tid >> 4;
+  P.g = tid & 15;
+  P.on = tid < kTwLanes;
+  P.base = st_base + 4 * (min(k, kMaxSeedsPerPass) * kMtN + P.g);
+  P.dummy = st_base + 4 * (kMaxSeedsPerPass * kMtN + (tid & 255));
 }
 
 __device__ __forceinline__ uint32_t lds_u32(const uint8_t* base, int off) {
@@ -335,38 +379,61 @@ __device__ __forceinline__ void lds_st(uint8_t* base, int off, uint32_t v) {
   *reinterpret_cast<uint32_t*>(base + off) = v;
 }
 
+// In-place twist of the windows (MT19937RNGEngine.h:164-175).  Word i of the new block
+// needs OLD words i and i+1 plus word i+397 (old, i < 227) or i-227 (new), so the 624
+// words form 3 dependency phases [0,227) [227,454) [454,624), and word 623 pairs with
+// the NEW word 0 (MT19937RNGEngine.h:174).  Each phase reads into registers, barriers,
+// then writes (word i reads word i+1, which another lane rewrites in the same phase).
 __device__ __forceinline__ void twist_all(uint8_t* lds, const TwistPlan& P) {
   uint32_t nv[kR12];
+  const int o = P.base;
   // phase 1: words [0, 227): m = x[i + 397] (old)
+  if (P.on) {
 #pragma unroll
-  for (int r = 0; r < kR12; r++) {
-    const int o = P.a12[r];
-    nv[r] = lds_u32(lds, o + 4 * kMtM) ^ mt_twist(lds_u32(lds, o), lds_u32(lds, o + 4));
+    for (int r = 0; r < kR12; r++)
+      nv[r] = lds_u32(lds, o + 64 * r + 4 * kMtM) ^ mt_twist(lds_u32(lds, o + 64 * r), lds_u32(lds, o + 64 * r + 4));
   }
   __syncthreads();
+  if (P.on) {
 #pragma unroll
-  for (int r = 0; r < kR12; r++) lds_st(lds, P.a12[r], nv[r]);
+    for (int r = 0; r < kR12; r++) {
+      const bool ok = r < kR12 - 1 || P.g + 16 * r < 227;
+      lds_st(lds, ok ? o + 64 * r : P.dummy, nv[r]);
+    }
+  }
   __syncthreads();
   // phase 2: words [227, 454): m = x[i - 227] (new, phase 1)
+  if (P.on) {
 #pragma unroll
-  for (int r = 0; r < kR12; r++) {
-    const int o = P.a12[r];
-    nv[r] = lds_u32(lds, o) ^ mt_twist(lds_u32(lds, o + 4 * 227), lds_u32(lds, o + 4 * 228));
+    for (int r = 0; r < kR12; r++)
+      nv[r] = lds_u32(lds, o + 64 * r) ^ mt_twist(lds_u32(lds, o + 64 * r + 4 * 227), lds_u32(lds, o + 64 * r + 4 * 228));
   }
   __syncthreads();
+  if (P.on) {
 #pragma unroll
-  for (int r = 0; r < kR12; r++) lds_st(lds, P.a12[r] + 4 * 227, nv[r]);
+    for (int r = 0; r < kR12; r++) {
+      const bool ok = r < kR12 - 1 || P.g + 16 * r < 227;
+      lds_st(lds, ok ? o + 64 * r + 4 * 227 : P.dummy, nv[r]);
+    }
+  }
   __syncthreads();
   // phase 3: words [454, 624): m = x[i - 227] (new, phase 2); word 623 pairs with new x[0]
+  if (P.on) {
 #pragma unroll
-  for (int r = 0; r < kR3; r++) {
-    const int o = P.a3[r];
-    const int ov = ((P.last3 >> r) & 1u) ? o - 4 * 169 - 4 * 455 : o;  // ov + 4*455 -> x[0] of this window
-    nv[r] = lds_u32(lds, o + 4 * 227) ^ mt_twist(lds_u32(lds, o + 4 * 454), lds_u32(lds, ov + 4 * 455));
+    for (int r = 0; r < kR3; r++) {
+      const bool last = (r == kR3 - 1) && (P.g + 16 * r == 169);
+      const int ov = last ? o - 4 * P.g - 4 * 455 : o + 64 * r;  // ov + 4*455 -> x[0] of this window
+      nv[r] = lds_u32(lds, o + 64 * r + 4 * 227) ^ mt_twist(lds_u32(lds, o + 64 * r + 4 * 454), lds_u32(lds, ov + 4 * 455));
+    }
   }
   __syncthreads();
+  if (P.on) {
 #pragma unroll
-  for (int r = 0; r < kR3; r++) lds_st(lds, P.a3[r] + 4 * 454, nv[r]);
+    for (int r = 0; r < kR3; r++) {
+      const bool ok = r < kR3 - 1 || P.g + 16 * r < 170;
+      lds_st(lds, ok ? o + 64 * r + 4 * 454 : P.dummy, nv[r]);
+    }
+  }
   __syncthreads();
 }
 
@@ -385,32 +452,53 @@ __device__ __forceinline__ void z_pair(const uint8_t* lds, uint32_t r1, uint32_t
     // normal_fill_16<BFloat16>: z = bf16(R[a] * C[b]) * 1 + 0 (std, mean).  R*C is exact
     // in f32 (8-bit x 8-bit significands) and fma(R, C, +0) turns -0 into +0 like "+ mean".
     const uint32_t a4 = mt_temper_u8x4(r1), b4 = mt_temper_u8x4(r2);
+#if FKS_DIAG >= 3  // diagnostics: no table lookups (wrong values)
+    const float r = __uint_as_float(a4 | 0x3f800000u);
+    const float2 cs = make_float2(__uint_as_float(b4 | 0x3f000000u), __uint_as_float(b4 | 0x3e000000u));
+#else
     const float r = *reinterpret_cast<const float*>(lds + a4);
     const float2 cs = *reinterpret_cast<const float2*>(lds + 1024 + 2 * b4);
+#endif
     z1 = rbf(__fmaf_rn(r, cs.x, 0.0f));
     z2 = rbf(__fmaf_rn(r, cs.y, 0.0f));
   }
 }
 
-// Seeds [k0, k0 + U): all LDS reads and z first (independent across seeds), then the
-// sequential per-element update chain in seed order.
-template <int DT, int MODE, int U>
-__device__ __forceinline__ void pair_group(const uint8_t* lds, int st_off, int k0, const float* g, float lr,
-                                           float wd, bool has_wd, float& p1, float& p2) {
-  uint32_t r1[U], r2[U];
+// All seeds of the pass: every state-word read of the block is issued up front
+// (latency hidden behind the z math of earlier seeds), z for every seed next, then
+// the sequential per-element update chain in seed order.
+template <int DT, int MODE, int NS>
+__device__ __forceinline__ void pair_all(const uint8_t* lds, int st_off, const float* g, float lr, float wd,
+                                         bool has_wd, float& p1, float& p2) {
+  uint32_t r1[NS], r2[NS];
 #pragma unroll
-  for (int u = 0; u < U; u++) {
-    r1[u] = lds_u32(lds, st_off + (k0 + u) * (kMtN * 4));
-    r2[u] = lds_u32(lds, st_off + (k0 + u) * (kMtN * 4) + 32);
+  for (int k = 0; k < NS; k++) {
+#if FKS_DIAG == 4  // diagnostics: every lane reads the same (broadcast) words (wrong values)
+    r1[k] = lds_u32(lds, kLdsTabBytes + k * (kMtN * 4));
+    r2[k] = lds_u32(lds, kLdsTabBytes + k * (kMtN * 4) + 32);
+#else
+    r1[k] = lds_u32(lds, st_off + k * (kMtN * 4));
+    r2[k] = lds_u32(lds, st_off + k * (kMtN * 4) + 32);
+#endif
   }
-  float z1[U], z2[U];
+  float z1[NS], z2[NS];
 #pragma unroll
-  for (int u = 0; u < U; u++) z_pair<DT>(lds, r1[u], r2[u], z1[u], z2[u]);
+  for (int k = 0; k < NS; k++) z_pair<DT>(lds, r1[k], r2[k], z1[k], z2[k]);
 #pragma unroll
-  for (int u = 0; u < U; u++) {
-    p1 = apply_one<DT>(p1, z1[u], g[k0 + u], lr, wd, has_wd, MODE);
-    p2 = apply_one<DT>(p2, z2[u], g[k0 + u], lr, wd, has_wd, MODE);
+  for (int k = 0; k < NS; k++) {
+    p1 = apply_one<DT>(p1, z1[k], g[k], lr, wd, has_wd, MODE);
+    p2 = apply_one<DT>(p2, z2[k], g[k], lr, wd, has_wd, MODE);
   }
+}
+
+// one seed (partial passes)
+template <int DT, int MODE>
+__device__ __forceinline__ void pair_one(const uint8_t* lds, int st_off, int k, float g, float lr, float wd,
+                                         bool has_wd, float& p1, float& p2) {
+  float z1, z2;
+  z_pair<DT>(lds, lds_u32(lds, st_off + k * (kMtN * 4)), lds_u32(lds, st_off + k * (kMtN * 4) + 32), z1, z2);
+  p1 = apply_one<DT>(p1, z1, g, lr, wd, has_wd, MODE);
+  p2 = apply_one<DT>(p2, z2, g, lr, wd, has_wd, MODE);
 }
 
 template <int DT, int MODE, bool FULL>
@@ -477,51 +565,253 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
     } else {
       seg_start = seg_end = INT64_MAX;
     }
+    // Drain here (rare: once per segment change), so the cached segment registers are
+    // never "possibly pending" later: otherwise every block's address computation would
+    // carry a vmcnt(0) that also waits for the previous block's stores.
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt/lgkmcnt untouched
   };
   load_seg();
 
   // software pipeline: block b+1's parameters are fetched before block b's Box-Muller
-  struct Slot { uint64_t ptr; int64_t e1; float lr, wd; bool wdf, on; float p1, p2; };
+  // Parameter traffic in pairs of ADJACENT elements: lane q (slot r = q%8 of its
+  // 16-block) owns elements j1 = 16m + r and j1 + 8; an even lane moves the pair
+  // (j1, j1+1), an odd lane the pair (j1+7, j1+8), and the two lanes swap the halves
+  // that belong to each other (one DPP op) -- one dword (bf16) / dwordx2 (f32) access
+  // per lane instead of two scattered ones.
+  const bool odd = (tid & 1) != 0;
+  constexpr int kEs = DT == FKS_F32 ? 4 : 2;
+  typedef typename Traits<DT>::Pair Pair;
+  struct Slot { uint64_t addr; float lr, wd; bool wdf, on; Pair raw; };
   auto fetch = [&](int64_t b) {
     Slot sl;
     const int64_t s1 = (int64_t)kMtN * b + j1;
     while (s1 >= seg_end) { cur++; load_seg(); }
     sl.on = lane_on && s1 >= seg_start;
-    sl.ptr = seg_ptr; sl.e1 = s1 - seg_start; sl.lr = seg_lr; sl.wd = seg_wd; sl.wdf = seg_wdf;
-    sl.p1 = 0.0f; sl.p2 = 0.0f;
-    if (MODE != kModeWriteZ && sl.on) {
-      sl.p1 = Traits<DT>::load(sl.ptr, sl.e1);
-      sl.p2 = Traits<DT>::load(sl.ptr, sl.e1 + 8);
-    }
+    sl.lr = seg_lr; sl.wd = seg_wd; sl.wdf = seg_wdf;
+    // off lanes read a valid dummy word, so the load is unconditional and its wait
+    // lands at first use, a block later
+    sl.addr = sl.on ? seg_ptr + (uint64_t)(s1 - seg_start + (odd ? 7 : 0)) * kEs : (uint64_t)(uintptr_t)a.states;
+    sl.raw = 0;
+    if (MODE != kModeWriteZ) sl.raw = Traits<DT>::load_pair(sl.addr);
     return sl;
   };
   Slot nxt = fetch(b0);
 
-#ifndef FKS_DIAG
-#define FKS_DIAG 0  // diagnostic builds only: 1 = twist only, 2 = Box-Muller/update only
-#endif
   for (int64_t b = b0; b < b1; b++) {
     Slot sl = nxt;
-    if (FKS_DIAG != 2) twist_all(lds, plan);  // the raw words of stream block b (sl's loads in flight meanwhile)
-    if (FKS_DIAG == 2) __syncthreads();
+    if (FKS_DIAG < 2 || FKS_DIAG == 5) twist_all(lds, plan);  // the raw words of stream block b
+    if (FKS_DIAG >= 2 && FKS_DIAG != 5) __syncthreads();
     if (b + 1 < b1) nxt = fetch(b + 1);
     if (sl.on && FKS_DIAG != 1) {
-      float p1 = sl.p1, p2 = sl.p2;
+      // even lane holds (p1, partner's p1), odd lane (partner's p2, p2)
+      const uint32_t keep = odd ? Traits<DT>::hi(sl.raw) : Traits<DT>::lo(sl.raw);
+      const uint32_t got = swap_adjacent(odd ? Traits<DT>::lo(sl.raw) : Traits<DT>::hi(sl.raw));
+      float p1 = Traits<DT>::cvt(odd ? got : keep), p2 = Traits<DT>::cvt(odd ? keep : got);
       if constexpr (FULL) {
-#pragma unroll
-        for (int k0 = 0; k0 + 4 <= kMaxSeedsPerPass; k0 += 4)
-          pair_group<DT, MODE, 4>(lds, st_off, k0, gk, sl.lr, sl.wd, sl.wdf, p1, p2);
-        constexpr int kTail = kMaxSeedsPerPass % 4;
-        if constexpr (kTail > 0)
-          pair_group<DT, MODE, kTail>(lds, st_off, kMaxSeedsPerPass - kTail, gk, sl.lr, sl.wd, sl.wdf, p1, p2);
+        pair_all<DT, MODE, kMaxSeedsPerPass>(lds, st_off, gk, sl.lr, sl.wd, sl.wdf, p1, p2);
       } else {
-        for (int k = 0; k < nseeds; k++) pair_group<DT, MODE, 1>(lds, st_off, k, gk, sl.lr, sl.wd, sl.wdf, p1, p2);
+        for (int k = 0; k < nseeds; k++) pair_one<DT, MODE>(lds, st_off, k, gk[k], sl.lr, sl.wd, sl.wdf, p1, p2);
       }
-      Traits<DT>::store(sl.ptr, sl.e1, p1);
-      Traits<DT>::store(sl.ptr, sl.e1 + 8, p2);
+      const uint32_t b1v = Traits<DT>::bits(p1), b2v = Traits<DT>::bits(p2);
+      const uint32_t back = swap_adjacent(odd ? b1v : b2v);  // even gets partner's p1, odd partner's p2
+      const Pair out = odd ? Traits<DT>::pack(back, b2v) : Traits<DT>::pack(b1v, back);
+#if FKS_DIAG == 6
+      if (p1 == 1234.5f && p2 == -99.25f)
+#endif
+      Traits<DT>::store_pair(sl.addr, out);
     }
     // no barrier here: the next twist's first barrier orders these LDS reads before
     // its first write
+  }
+}
+
+// ------------------------------------------------------------------ irregular kernel
+// Everything the fast kernel does not take (DESIGN.md "Irregular layouts"):
+//   * runs of whole 16-blocks at any stream phase (a tensor after a ragged one, a
+//     ragged tensor's head with its overwritten elements masked, its 16-word tail
+//     recompute, f16 tensors, parameters not 2-element aligned), and
+//   * single elements of numel < 16 tensors (serial normal_distribution<double>,
+//     DistributionsHelper.h:189-221, with the cached second sample).
+// A work item is handled in the MT block holding its LAST word; its first words may
+// lie up to 15 words back, in the previous block, so every seed window carries the
+// previous block's last 16 raw words in front of it: [carry 16 | 624].
+__constant__ float c_tab_f16[3 * 2048];  // R | C | S of the 11-bit f16 uniforms
+
+constexpr int kIrrCarry = 16;
+constexpr int kIrrWin = kIrrCarry + kMtN;  // words per seed window
+
+__device__ __forceinline__ uint32_t win_word(const uint32_t* win, int k, int w) {  // w in [-16, 624)
+  return win[k * kIrrWin + kIrrCarry + w];
+}
+
+// in-place twist of every window, phase PH of 3 (i in [0,227) / [227,454) / [454,624));
+// phase 0 also saves the old words 608..623 as the next block's carry
+template <int PH>
+__device__ __forceinline__ void irr_twist_phase(uint32_t* win, int nseeds, int tid) {
+  constexpr int lo = PH == 0 ? 0 : (PH == 1 ? 227 : 454);
+  constexpr int hi = PH == 0 ? 227 : (PH == 1 ? 454 : kMtN);
+  constexpr int len = hi - lo;
+  constexpr int per = (kMaxSeedsPerPass * len + kApplyThreads - 1) / kApplyThreads;
+  uint32_t v[per];
+#pragma unroll
+  for (int j = 0; j < per; j++) {
+    const int idx = tid + j * kApplyThreads;
+    if (idx < nseeds * len) {
+      const int k = idx / len, i = lo + idx % len;
+      const uint32_t* w = win + k * kIrrWin + kIrrCarry;
+      const uint32_t nx = i == kMtN - 1 ? w[0] : w[i + 1];
+      const uint32_t m = i < kMtN - kMtM ? w[i + kMtM] : w[i - (kMtN - kMtM)];
+      v[j] = m ^ mt_twist(w[i], nx);
+    }
+  }
+  uint32_t cv = 0;
+  if (PH == 0 && tid < nseeds * kIrrCarry) cv = win[(tid / kIrrCarry) * kIrrWin + kIrrCarry + kMtN - kIrrCarry + tid % kIrrCarry];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < per; j++) {
+    const int idx = tid + j * kApplyThreads;
+    if (idx < nseeds * len) win[(idx / len) * kIrrWin + kIrrCarry + lo + idx % len] = v[j];
+  }
+  if (PH == 0 && tid < nseeds * kIrrCarry) win[(tid / kIrrCarry) * kIrrWin + tid % kIrrCarry] = cv;
+  __syncthreads();
+}
+
+// z pair from two raw words, any dtype (f16 through its 11-bit tables in constant memory)
+template <int DT>
+__device__ __forceinline__ void irr_z_pair(const uint8_t* lds, uint32_t r1, uint32_t r2, float& z1, float& z2) {
+  if constexpr (DT == FKS_F16) {
+    const uint32_t a = mt_temper(r1) & 0x7FFu, b = mt_temper(r2) & 0x7FFu;
+    z1 = rhf(__fmaf_rn(c_tab_f16[a], c_tab_f16[2048 + b], 0.0f));
+    z2 = rhf(__fmaf_rn(c_tab_f16[a], c_tab_f16[4096 + b], 0.0f));
+  } else {
+    z_pair<DT>(lds, r1, r2, z1, z2);
+  }
+}
+
+template <int DT, int MODE>
+__device__ __forceinline__ void irr_run_lane(const uint8_t* lds, const uint32_t* win, const IrrArgs& a, const DevRun& R,
+                                             int64_t e1, int w1) {
+  using TR = Traits<DT>;
+  const bool on1 = e1 < R.limit, on2 = e1 + 8 < R.limit;
+  float p1 = 0.0f, p2 = 0.0f;
+  if (MODE != kModeWriteZ) {
+    if (on1) p1 = TR::load(R.ptr, e1);
+    if (on2) p2 = TR::load(R.ptr, e1 + 8);
+  }
+  const bool has_wd = (R.flags & FKS_HAS_WD) != 0;
+  const float* g = a.g + (size_t)DT * a.gstride;
+  for (int k = 0; k < a.nseeds; k++) {
+    float z1, z2;
+    irr_z_pair<DT>(lds, win_word(win, k, w1), win_word(win, k, w1 + 8), z1, z2);
+    p1 = apply_one<DT>(p1, z1, g[k], R.lr, R.wd, has_wd, MODE);
+    p2 = apply_one<DT>(p2, z2, g[k], R.lr, R.wd, has_wd, MODE);
+  }
+  if (on1) TR::store(R.ptr, e1, p1);
+  if (on2) TR::store(R.ptr, e1 + 8, p2);
+}
+
+__device__ __forceinline__ double u53(uint32_t hi, uint32_t lo) {  // uniform_real_distribution<double>
+  const uint64_t x = (((uint64_t)hi << 32) | lo) & ((1ull << 53) - 1);
+  return (double)x * (1.0 / 9007199254740992.0);
+}
+
+template <int DT, int MODE>
+__device__ __forceinline__ void irr_tiny_lane(const uint32_t* win, const IrrArgs& a, const DevTiny& T, int w) {
+  using TR = Traits<DT>;
+  float p = MODE != kModeWriteZ ? TR::load(T.ptr, 0) : 0.0f;
+  const bool has_wd = (T.flags & FKS_HAS_WD) != 0;
+  const bool sin_half = (T.flags & kTinySin) != 0;
+  const float* g = a.g + (size_t)DT * a.gstride;
+  for (int k = 0; k < a.nseeds; k++) {
+    const double u1 = u53(mt_temper(win_word(win, k, w)), mt_temper(win_word(win, k, w + 1)));
+    const double u2 = u53(mt_temper(win_word(win, k, w + 2)), mt_temper(win_word(win, k, w + 3)));
+    const double r = sqrt(-2.0 * log1p(-u2));
+    const double theta = 2.0 * 3.14159265358979323846 * u1;
+    const double v = (sin_half ? r * sin(theta) : r * cos(theta)) * 1.0 + 0.0;
+    const float zf = (float)v;  // static_cast<scalar_t>(double): via float for bf16 / f16
+    const float z = DT == FKS_F32 ? zf : TR::rnd(zf);
+    p = apply_one<DT>(p, z, g[k], T.lr, T.wd, has_wd, MODE);
+  }
+  TR::store(T.ptr, 0, p);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kApplyThreads) void fks_irregular_kernel(IrrArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
+  uint32_t* win = reinterpret_cast<uint32_t*>(lds + kLdsTabBytes);
+  const int tid = threadIdx.x;
+  const int c = blockIdx.x;
+  const int nseeds = a.nseeds;
+  const int64_t b0 = a.chunk_lo[c], b1 = a.chunk_hi[c];
+  {
+    float* tabR = reinterpret_cast<float*>(lds);
+    float2* tabCS = reinterpret_cast<float2*>(lds + 1024);
+    for (int i = tid; i < 256; i += kApplyThreads) {
+      tabR[i] = c_tab_bf16[i];
+      tabCS[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
+    }
+  }
+  for (int idx = tid; idx < nseeds * kMtN; idx += kApplyThreads) {
+    const int k = idx / kMtN, i = idx - k * kMtN;
+    win[k * kIrrWin + kIrrCarry + i] = a.states[((size_t)k * a.nchunks + c) * kMtN + i];
+  }
+  // first run whose last word is in or after block b0; first single element likewise
+  int ri, ti;
+  {
+    int lo = 0, hi = a.nruns;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (a.runs[mid].start + a.runs[mid].numel - 1 < (int64_t)kMtN * b0) lo = mid + 1; else hi = mid;
+    }
+    ri = lo;
+    lo = 0, hi = a.ntiny;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (a.tiny[mid].word + 3 < (int64_t)kMtN * b0) lo = mid + 1; else hi = mid;
+    }
+    ti = lo;
+  }
+  __syncthreads();
+  const int m = tid >> 3, r8 = tid & 7;
+  for (int64_t b = b0; b < b1; b++) {
+    irr_twist_phase<0>(win, nseeds, tid);
+    irr_twist_phase<1>(win, nseeds, tid);
+    irr_twist_phase<2>(win, nseeds, tid);
+    const int64_t base = (int64_t)kMtN * b, end = base + kMtN;
+    // runs with a 16-block ending in this block (disjoint, sorted: a contiguous range)
+    while (ri < a.nruns && a.runs[ri].start + 15 < end) {
+      const DevRun R = a.runs[ri];
+      const int ph = (int)(R.start & 15);
+      const int64_t s0 = base + 16 * m + (ph ? ph - 16 : 0);  // this lane's 16-block start
+      if (tid < kMtN / 2 && s0 >= R.start && s0 < R.start + R.numel) {
+        const int64_t e1 = s0 - R.start + r8;
+        const int w1 = (int)(s0 - base) + r8;
+        switch (R.dtype) {
+          case FKS_F32: irr_run_lane<FKS_F32, MODE>(lds, win, a, R, e1, w1); break;
+          case FKS_BF16: irr_run_lane<FKS_BF16, MODE>(lds, win, a, R, e1, w1); break;
+          default: irr_run_lane<FKS_F16, MODE>(lds, win, a, R, e1, w1); break;
+        }
+      }
+      if (R.start + R.numel - 1 < end) ri++; else break;
+    }
+    // single elements whose draw pair ends in this block (sorted: a prefix from ti)
+    for (;;) {
+      const int idx = ti + tid;
+      const bool mine = idx < a.ntiny && a.tiny[idx].word + 3 < end;
+      if (mine) {
+        const DevTiny T = a.tiny[idx];
+        const int w = (int)(T.word - base);
+        switch (T.dtype) {
+          case FKS_F32: irr_tiny_lane<FKS_F32, MODE>(win, a, T, w); break;
+          case FKS_BF16: irr_tiny_lane<FKS_BF16, MODE>(win, a, T, w); break;
+          default: irr_tiny_lane<FKS_F16, MODE>(win, a, T, w); break;
+        }
+      }
+      const int n = __syncthreads_count(mine);
+      ti += n;
+      if (n < kApplyThreads) break;
+    }
   }
 }
 
@@ -538,16 +828,23 @@ int device_cu_count() {
 }
 
 static int ensure_tables() {
-  static int done = 0;  // per process; the constant symbol lives in this code object
+  static int done = 0;  // per process; the constant symbols live in this code object
   if (done) return 0;
   const Tables& t = tables();
-  float buf[768];
+  static float buf[3 * 2048];
   for (int i = 0; i < 256; i++) {
     buf[i] = t.r_bf16[i];
     buf[256 + i] = t.c_bf16[i];
     buf[512 + i] = t.s_bf16[i];
   }
-  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_tab_bf16), buf, sizeof(buf), 0, hipMemcpyHostToDevice);
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_tab_bf16), buf, sizeof(float) * 768, 0, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return (int)e;
+  for (int i = 0; i < 2048; i++) {
+    buf[i] = t.r_f16[i];
+    buf[2048 + i] = t.c_f16[i];
+    buf[4096 + i] = t.s_f16[i];
+  }
+  e = hipMemcpyToSymbol(HIP_SYMBOL(c_tab_f16), buf, sizeof(buf), 0, hipMemcpyHostToDevice);
   if (e != hipSuccess) return (int)e;
   done = 1;
   return 0;
@@ -600,6 +897,33 @@ int launch_apply(int dtype, const ApplyArgs& a, void* stream) {
     case FKS_BF16 * 4 + kModeUpdate: return launch_apply_t<FKS_BF16, kModeUpdate>(a, stream);
     case FKS_BF16 * 4 + kModePerturb: return launch_apply_t<FKS_BF16, kModePerturb>(a, stream);
     case FKS_BF16 * 4 + kModeWriteZ: return launch_apply_t<FKS_BF16, kModeWriteZ>(a, stream);
+    default: return -FKS_ENOTSUP;
+  }
+}
+
+template <int MODE>
+static int launch_irregular_m(const IrrArgs& a, void* stream) {
+  const size_t lds = (size_t)kLdsTabBytes + sizeof(uint32_t) * kIrrWin * (size_t)kMaxSeedsPerPass;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fks_irregular_kernel<MODE>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((fks_irregular_kernel<MODE>), dim3((unsigned)a.nchunks), dim3(kApplyThreads), lds,
+                     (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+int launch_irregular(const IrrArgs& a, void* stream) {
+  if (a.nseeds < 1 || a.nseeds > kMaxSeedsPerPass) return -FKS_EINVAL;
+  int e = ensure_tables();
+  if (e) return e;
+  switch (a.mode) {
+    case kModeUpdate: return launch_irregular_m<kModeUpdate>(a, stream);
+    case kModePerturb: return launch_irregular_m<kModePerturb>(a, stream);
+    case kModeWriteZ: return launch_irregular_m<kModeWriteZ>(a, stream);
     default: return -FKS_ENOTSUP;
   }
 }

@@ -52,6 +52,31 @@ struct DevSeg {
 };
 static_assert(sizeof(DevSeg) == 40, "DevSeg layout");
 
+// Irregular work (fks_irregular_kernel): a run of whole 16-blocks at any stream phase ...
+struct DevRun {
+  int64_t start;   // stream word of the run's first 16-block
+  int64_t numel;   // 16 * (16-blocks in the run)
+  uint64_t ptr;    // device address of the run's element 0
+  int64_t limit;   // elements [limit, numel) are not written (a ragged head, see make_layout)
+  float lr;
+  float wd;
+  uint32_t flags;  // FKS_HAS_WD
+  int32_t dtype;
+};
+static_assert(sizeof(DevRun) == 48, "DevRun layout");
+
+// ... and one element of a numel < 16 tensor (serial normal_distribution<double>)
+constexpr uint32_t kTinySin = 1u << 8;  // the element takes the pair's cached r*sin value
+struct DevTiny {
+  int64_t word;    // stream word of its Box-Muller pair (two random64 draws = 4 words)
+  uint64_t ptr;    // device address of the element
+  float lr;
+  float wd;
+  uint32_t flags;  // FKS_HAS_WD | kTinySin
+  int32_t dtype;
+};
+static_assert(sizeof(DevTiny) == 32, "DevTiny layout");
+
 constexpr int kApplyThreads = 320;  // 312 Box-Muller pairs per 624-word block + 8 idle lanes
 #ifndef FKS_APPLY_WG_PER_CU
 #define FKS_APPLY_WG_PER_CU 3
@@ -75,6 +100,21 @@ struct ApplyArgs {
   int32_t mode;
 };
 
+struct IrrArgs {
+  const uint32_t* states;       // [nseeds][nchunks][624]
+  const float* g;               // [3][gstride]: per-dtype multipliers of this pass's seeds
+  const DevRun* runs;           // sorted by start (disjoint)
+  const DevTiny* tiny;          // sorted by word
+  const int64_t* chunk_lo;      // [nchunks] chunk c twists MT blocks [chunk_lo[c], chunk_hi[c])
+  const int64_t* chunk_hi;
+  int64_t gstride;
+  int32_t nruns;
+  int32_t ntiny;
+  int32_t nchunks;
+  int32_t nseeds;
+  int32_t mode;
+};
+
 struct JumpArgs {
   const uint64_t* seeds;        // [nseeds]
   const uint64_t* polys;        // [nchunks][312] t^(624*b-1) mod phi (unused for b == 0)
@@ -87,6 +127,7 @@ struct JumpArgs {
 // launchers (fks_device.hip); return hipError_t as int
 int launch_jump(const JumpArgs& a, int nseeds, void* stream);
 int launch_apply(int dtype, const ApplyArgs& a, void* stream);
+int launch_irregular(const IrrArgs& a, void* stream);
 int device_cu_count();
 
 }  // namespace fks

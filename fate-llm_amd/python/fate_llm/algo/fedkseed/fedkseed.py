@@ -1,0 +1,151 @@
+"""Drop-in for python/fate_llm/algo/fedkseed/fedkseed.py (FATE-LLM 2.2.0).
+
+Arbiter side (``Trainer``, reference :17-85): per round, recompute the seed-sampling
+probabilities from every seed's directional-derivative history, send
+``(should_exit, {seed_candidates, seed_probabilities, direction_derivative_sum})`` to
+every client, then fold the clients' histories into the history and the cumulative
+float64 sums.  Only K-sized scalars move; nothing here touches parameters.
+
+Client side (``ClientTrainer``, reference :88-158): per round, rebuild the model from
+``model_0`` plus the cumulative (seed, sum) list -- the K-seed reconstruct, one
+``zo_utils.reconstruct_`` call on the MI355X codec instead of K Python-level
+``directional_derivative_step`` calls -- then run local KSeedZO training and return
+the directional-derivative history.
+
+The federation context is duck-typed (``ctxs_range``, ``guest``, ``hosts``,
+``arbiter.put/get``), so ``fate.arch`` is not a dependency of this package.
+"""
+import copy
+import logging
+from dataclasses import dataclass, field
+from typing import Dict, List, Mapping, Optional
+
+import torch
+
+from .args import KSeedTrainingArguments
+from .pytorch_utils import get_optimizer_parameters_grouped_with_decay
+from .zo_utils import get_even_seed_probabilities, probability_from_amps, reconstruct_
+
+logger = logging.getLogger(__name__)
+
+
+class Trainer:
+    """FedKSeed arbiter (reference fedkseed.py:17-85)."""
+
+    def __init__(self, ctx, seed_candidates: torch.LongTensor, args, fedkseed_args):
+        self.ctx = ctx
+        self.args = args
+        self.fedkseed_args = fedkseed_args
+        self.seed_candidates = seed_candidates
+        self.k = len(seed_candidates)
+        self.model = None
+
+    @staticmethod
+    def get_clients(ctx) -> list:
+        """The guest, then every host (a context without hosts has only the guest)."""
+        clients = [ctx.guest]
+        hosts = getattr(ctx, "hosts", None)
+        if hosts:
+            clients.extend(hosts)
+        return clients
+
+    def load_model(self):
+        raise NotImplementedError
+
+    def _probabilities(self, history: Dict[int, List[float]], first: bool):
+        if first:
+            return get_even_seed_probabilities(self.k)
+        return probability_from_amps([history[s.item()] for s in self.seed_candidates],
+                                     self.fedkseed_args.bias_loss_clip)
+
+    def train(self):
+        history: Dict[int, List[float]] = {s.item(): [self.fedkseed_args.grad_initial] for s in self.seed_candidates}
+        # one dict object for the whole run, updated in place after every round (the
+        # reference hands the same object to every put)
+        sums: Optional[Dict[int, float]] = None
+        probs = None
+        for _, sub_ctx in self.ctx.ctxs_range(self.fedkseed_args.num_aggregations):
+            probs = self._probabilities(history, first=probs is None)
+            payload = {"seed_candidates": self.seed_candidates, "seed_probabilities": probs,
+                       "direction_derivative_sum": sums}
+            clients = self.get_clients(sub_ctx)
+            for client in clients:
+                client.put("train_once", (False, payload))
+            if sums is None:
+                sums = {s.item(): 0.0 for s in self.seed_candidates}
+            for client in clients:
+                for seed, values in client.get("direction_derivative_history").items():
+                    seed = int(seed)
+                    history.setdefault(seed, []).extend(values)
+                    # python float sum of the new values, then one float64 add; a seed
+                    # outside the candidates raises KeyError, as in the reference
+                    sums[seed] += sum(values)
+            if self.should_stop():
+                break
+
+    def should_stop(self) -> bool:
+        return False
+
+    def evaluate(self):
+        pass
+
+
+class ClientTrainer:
+    """FedKSeed client (reference fedkseed.py:88-158)."""
+
+    def __init__(self, ctx, model, fedkseed_args, training_args, train_dataset, eval_dataset, data_collator,
+                 tokenizer):
+        self.ctx = ctx
+        self.fedkseed_args = fedkseed_args
+        self.training_args = training_args
+        self.data_collator = data_collator
+        self.train_dataset = train_dataset
+        self.eval_dataset = eval_dataset
+        self.tokenizer = tokenizer
+        self.weight_decay = training_args.weight_decay
+        self.model_0 = model
+
+    def train(self):
+        for i, sub_ctx in self.ctx.ctxs_range(self.fedkseed_args.num_aggregations):
+            logger.info(f"training loop started: {i}")
+            should_exit, kwargs = sub_ctx.arbiter.get("train_once")
+            if should_exit:
+                break
+            history = self.train_once(kwargs["seed_candidates"], kwargs["seed_probabilities"],
+                                      kwargs["direction_derivative_sum"])
+            sub_ctx.arbiter.put("direction_derivative_history", history)
+
+    def reconstruct(self, direction_derivative_sum: Optional[Mapping[int, float]]):
+        """model_0 + every accumulated (seed, sum) step, in the dict's insertion order,
+        zero sums skipped (reference :130-141), on the training device."""
+        model = copy.deepcopy(self.model_0)
+        model.to(self.training_args.device)
+        if direction_derivative_sum is not None:
+            groups = get_optimizer_parameters_grouped_with_decay(model, self.weight_decay)
+            reconstruct_(groups, list(direction_derivative_sum.keys()), list(direction_derivative_sum.values()),
+                         lr=self.training_args.learning_rate, weight_decay=self.training_args.weight_decay)
+        return model
+
+    def train_once(self, seed_candidates, seed_probabilities, direction_derivative_sum) -> Mapping[int, List[float]]:
+        from .trainer import KSeedZOExtendedTrainer  # needs transformers; the codec does not
+
+        model = self.reconstruct(direction_derivative_sum)
+        trainer = KSeedZOExtendedTrainer(
+            model=model, training_args=self.training_args, kseed_args=self.fedkseed_args, tokenizer=self.tokenizer,
+            data_collator=self.data_collator, train_dataset=self.train_dataset, eval_dataset=self.eval_dataset)
+        trainer.configure_seed_candidates(seed_candidates, seed_probabilities)
+        trainer.train()
+        if self.eval_dataset is not None:
+            logger.info(f"evaluate: {trainer.evaluate()}")
+        return trainer.get_directional_derivative_history()
+
+
+@dataclass
+class FedKSeedTrainingArguments(KSeedTrainingArguments):
+    """KSeed options plus the federation's (same fields and defaults as the reference)."""
+
+    num_aggregations: int = field(default=10, metadata={"help": "The number of aggregations to perform."})
+    bias_loss_clip: float = field(default=1000.0, metadata={"help": "The bias loss clip value."})
+    grad_initial: float = field(
+        default=0.0, metadata={"help": "The initial value for the directional derivative history."}
+    )

@@ -97,6 +97,14 @@ int fks_directional_step_shard(const fks_tensor* t, int32_t nt, const uint64_t* 
                                int32_t k, int32_t value_kind, int32_t shard, int32_t nshards, void* workspace,
                                size_t ws_bytes, void* stream);
 
+/* Host-only census of element sharding (no device work): the stream words
+ * [word_range[0], word_range[1]) shard `shard` of `nshards` owns, and per tensor the
+ * number of elements fks_directional_step_shard writes for it (`written`, nt entries;
+ * either output may be NULL).  Over all shards every element of a non-frozen tensor
+ * is written exactly once. */
+int fks_shard_census(const fks_tensor* t, int32_t nt, int32_t shard, int32_t nshards, int64_t* word_range,
+                     int64_t* written);
+
 /* Number of 32-bit generator words the tensor list consumes per seed (its stream length). */
 int fks_stream_length(const fks_tensor* t, int32_t nt, int64_t* words);
 

@@ -13,8 +13,8 @@ from oracle import fks_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-DTC = {"float32": O.F32, "bfloat16": O.BF16}
-TD = {"float32": torch.float32, "bfloat16": torch.bfloat16}
+DTC = {"float32": O.F32, "bfloat16": O.BF16, "float16": O.F16}
+TD = {"float32": torch.float32, "bfloat16": torch.bfloat16, "float16": torch.float16}
 
 
 def _dev():
@@ -24,15 +24,16 @@ def _dev():
 
 
 def to_np(t: torch.Tensor) -> np.ndarray:
+    """bits as stored in the golden files: uint16 for bf16/f16, float32 for f32"""
     t = t.detach().contiguous().cpu()
-    if t.dtype == torch.bfloat16:
+    if t.dtype in (torch.bfloat16, torch.float16):
         return t.view(torch.int16).numpy().view(np.uint16).copy()
     return t.numpy().copy()
 
 
 def from_np(a: np.ndarray, dtype: str, dev) -> torch.Tensor:
-    if dtype == "bfloat16":
-        return torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16).to(dev)
+    if dtype in ("bfloat16", "float16"):
+        return torch.from_numpy(a.view(np.int16).copy()).view(TD[dtype]).to(dev)
     return torch.from_numpy(a.copy()).to(dev)
 
 
@@ -76,11 +77,11 @@ def _gpu_reconstruct(arrays, dtype, lrs, wds, seeds, scalars, tensor_value=False
     return [to_np(t) for t in ts]
 
 
-REGULAR_CASES = ["f32_wd", "f32_nowd", "bf16_wd", "bf16_nowd", "f32_sticky", "bf16_sticky", "f32_edge", "bf16_nan",
-                 "f32_wdnone"]
+ALL_CASES = ["f32_wd", "f32_nowd", "bf16_wd", "bf16_nowd", "f16_wd", "f32_ragged", "bf16_ragged", "f32_sticky",
+             "bf16_sticky", "f32_edge", "bf16_nan", "f32_k4096", "bf16_k4096", "f32_wdnone"]
 
 
-@pytest.mark.parametrize("name", REGULAR_CASES)
+@pytest.mark.parametrize("name", ALL_CASES)
 def test_reconstruct_golden(golden, cases, name):
     """The train_once reconstruct loop through the drop-in zo_utils, vs the reference."""
     from fate_llm.algo.fedkseed import zo_utils
@@ -193,10 +194,122 @@ def test_perturb_sequence_vs_oracle(dtype):
         assert_bitwise(to_np(t), a, dtype, f"mixed-eps tensor {i}")
 
 
-def test_zeroth_order_optimizer_end_to_end():
-    """KSeedZerothOrderOptimizer steps with a device-independent closure, vs the golden
-    run of the reference optimizer on CPU (regular layout only: float32 TinyLM)."""
-    pytest.skip("golden optimizer fixtures use a ragged layout; covered once the generic path lands")
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_zeroth_order_optimizer_golden(golden, cases, dtype):
+    """ZerothOrderOptimizer on the ragged TinyLM (tiny, ragged and 7-element tensors, a
+    frozen tensor kept in its group): three perturbations, then zeroth_order_step with
+    pre-set losses -- every snapshot bit-exact against the reference run."""
+    from fate_llm.algo.fedkseed.optimizer import ZerothOrderOptimizer
+    dev = _dev()
+    case = cases["optimizer"][dtype]
+    z = golden(f"optimizer_{dtype}.npz")
+    order = [n for grp in case["groups"] for n in grp]
+    params = {n: torch.nn.Parameter(from_np(z[f"s0/{n}"].reshape(-1), dtype, dev),
+                                    requires_grad=case["requires_grad"][n]) for n in order}
+    groups = [{"params": [params[n] for n in grp], "weight_decay": wd}
+              for grp, wd in zip(case["groups"], (0.0, case["wd"]))]
+    opt = ZerothOrderOptimizer(groups, lr=case["lr"], eps=case["eps"], weight_decay=case["wd"], grad_clip=-100.0)
+    for step, sf in enumerate((1.0, -2.0, 1.0), start=1):
+        opt.random_perturb_parameters(case["perturb_seed"], scaling_factor=sf)
+        torch.cuda.synchronize()
+        for n in order:
+            assert_bitwise(to_np(params[n].data), z[f"s{step}/{n}"], dtype, f"perturb {step}/{n}")
+    losses = iter([torch.tensor(x) for x in case["losses"]])
+    g, _, _ = opt.zeroth_order_step(case["step_seed"], lambda: next(losses))
+    torch.cuda.synchronize()
+    assert float(g) == float(z["g"][0])
+    for n in order:
+        assert_bitwise(to_np(params[n].data), z[f"s4/{n}"], dtype, f"zo step/{n}")
+
+
+# ----------------------------------------------------------------------------- irregular layouts
+IRREGULAR_SHAPES = [3, 48, 7, 185, 37, 5, 1, 336, 1, 15, 17, 624 * 2 + 5, 2, 4096, 13, 31, 16, 9]
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16", "float16"])
+def test_irregular_layout_vs_oracle(dtype):
+    """Tiny tensors (serial double path with the cached sample carried across tensors),
+    ragged tensors (tail recompute), tensors at odd stream phases and 16-aligned ones
+    interleaved; K=23 covers a full and a partial seed pass."""
+    shapes = IRREGULAR_SHAPES
+    arrays = rand_params(shapes, dtype, seed=7)
+    gg = torch.Generator().manual_seed(8)
+    seeds = torch.randint(0, 2**32, (23,), generator=gg).tolist()
+    vals = (torch.randn(23, generator=gg, dtype=torch.float64) * 20).tolist()
+    lrs = [1e-3] * len(shapes)
+    wds = [0.01 if i % 3 else 0.0 for i in range(len(shapes))]
+    wds[4] = None
+    got = _gpu_reconstruct(arrays, dtype, lrs, wds, seeds, vals)
+    O.reconstruct(arrays, [DTC[dtype]] * len(arrays), lrs, wds, seeds, vals)
+    for i, (a, b) in enumerate(zip(got, arrays)):
+        assert_bitwise(a, b, dtype, f"tensor {i} (numel {shapes[i]})")
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16", "float16"])
+def test_irregular_normal_stream_vs_oracle(dtype):
+    """z itself (torch.normal per tensor, one seed) over the irregular layout."""
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    ts = [torch.empty(n, dtype=TD[dtype], device=dev) for n in IRREGULAR_SHAPES]
+    codec.normal_(ts, 2718281828)
+    gen = O.Generator(2718281828)
+    for n, t in zip(IRREGULAR_SHAPES, ts):
+        assert_bitwise(to_np(t), gen.normal(n, DTC[dtype]), dtype, f"n {n}")
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_phase_shifted_large_tensor_multichunk(dtype):
+    """A 5-element tensor first shifts every later tensor to stream phase 12: 1.5M params
+    on the irregular kernel across many chunks, every chunk start a GF(2) jump."""
+    shapes = [5, 2**20 + 2**19, 40, 2**16]
+    arrays = rand_params(shapes, dtype, seed=9)
+    seeds, vals = [5, 6, 7], [1.5, -2.5, 30.0]
+    got = _gpu_reconstruct(arrays, dtype, [1e-3] * 4, [0.01] * 4, seeds, vals)
+    O.reconstruct(arrays, [DTC[dtype]] * 4, [1e-3] * 4, [0.01] * 4, seeds, vals)
+    for i, (a, b) in enumerate(zip(got, arrays)):
+        assert_bitwise(a, b, dtype, f"tensor {i}")
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_odd_element_offsets(dtype):
+    """Views of one flat buffer at odd element offsets (the fast kernel moves aligned
+    element pairs; these go through the irregular kernel)."""
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    shapes = [4096, 160, 2**15]
+    arrays = rand_params(shapes, dtype, seed=10)
+    flat = torch.zeros(1 + sum(shapes) + 3, dtype=TD[dtype], device=dev)
+    views, off = [], 1
+    for a in arrays:
+        v = flat[off:off + a.size]
+        v.copy_(from_np(a, dtype, dev))
+        views.append(v)
+        off += a.size + 1
+    specs = [codec.ParamSpec(v, lr=1e-3, weight_decay=0.01) for v in views]
+    codec.directional_step(specs, [77, 78], [2.0, -3.0])
+    O.reconstruct(arrays, [DTC[dtype]] * 3, [1e-3] * 3, [0.01] * 3, [77, 78], [2.0, -3.0])
+    for i, (v, a) in enumerate(zip(views, arrays)):
+        assert_bitwise(to_np(v), a, dtype, f"view {i}")
+
+
+@pytest.mark.parametrize("nshards", [2, 3, 8])
+def test_element_shards_equal_whole(nshards):
+    """Element sharding (what each rank of bench.py / the N-GPU reconstruct runs): the
+    union of all shards equals the unsharded reconstruct bit for bit, irregular work
+    included."""
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    shapes = [2**18, 37, 3, 2**16 + 16, 185, 624 * 40]
+    arrays = rand_params(shapes, "bfloat16", seed=11)
+    seeds, vals = list(range(100, 125)), [float(i) - 12.5 for i in range(25)]
+    whole = _gpu_reconstruct(arrays, "bfloat16", [1e-3] * 6, [0.01] * 6, seeds, vals)
+    ts = [from_np(a, "bfloat16", dev) for a in arrays]
+    specs = [codec.ParamSpec(t, lr=1e-3, weight_decay=0.01) for t in ts]
+    for r in range(nshards):
+        codec.directional_step(specs, seeds, vals, shard=r, nshards=nshards)
+    torch.cuda.synchronize()
+    for i, (t, w) in enumerate(zip(ts, whole)):
+        assert_bitwise(to_np(t), w, "bfloat16", f"tensor {i}")
 
 
 def test_cpu_tensors_rejected():
