@@ -54,6 +54,14 @@ __device__ __forceinline__ uint32_t mt_temper_u8x4(uint32_t y) {
   return __builtin_amdgcn_bitop3_b32(y << 2, y >> 16, 0x3FCu, kXorMask);
 }
 
+// the same bits times 8 (a byte offset into a table of f32 pairs)
+__device__ __forceinline__ uint32_t mt_temper_u8x8(uint32_t y) {
+  y ^= (y >> 11);
+  y = __builtin_amdgcn_bitop3_b32(y, y << 7, 0x9d2c5680u, kXorAnd);
+  y = __builtin_amdgcn_bitop3_b32(y, y << 15, 0xefc60000u, kXorAnd);
+  return __builtin_amdgcn_bitop3_b32(y << 3, y >> 15, 0x7F8u, kXorMask);
+}
+
 // ------------------------------------------------------------------ rounding
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
@@ -71,6 +79,10 @@ __device__ __forceinline__ float rbf(float x) {
 #endif
 }
 __device__ __forceinline__ float rhf(float x) {  // RNE to f16 and back
+  // The empty asm pins x as an f32 VALUE: without it the backend folds the producing
+  // f32 multiply into v_fma_mixlo_f16 (one rounding of the exact product straight to
+  // f16), while c10::Half rounds the f32 product first (double rounding).
+  asm volatile("" : "+v"(x));
   return static_cast<float>(static_cast<_Float16>(x));
 }
 
@@ -372,11 +384,28 @@ __device__ __forceinline__ void twist_plan(TwistPlan& P, int tid, int st_base) {
   P.dummy = st_base + 4 * (kMaxSeedsPerPass * kMtN + (tid & 255));
 }
 
-__device__ __forceinline__ uint32_t lds_u32(const uint8_t* base, int off) {
-  return *reinterpret_cast<const uint32_t*>(base + off);
-}
-__device__ __forceinline__ void lds_st(uint8_t* base, int off, uint32_t v) {
-  *reinterpret_cast<uint32_t*>(base + off) = v;
+// LDS accessors by byte offset.  The apply kernel's only LDS is its dynamic block,
+// which starts at LDS address 0 (no static __shared__; checked at kernel entry), so an
+// offset IS the address: immediates fold into ds_read/ds_write and no base add is
+// spent per access.
+typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+typedef __attribute__((address_space(3))) float lds_f32_t;
+typedef __attribute__((address_space(3))) f32x2_t lds_f32x2_t;
+__device__ __forceinline__ uint32_t lds_u32(const uint8_t*, int off) { return *(const lds_u32_t*)(size_t)off; }
+__device__ __forceinline__ void lds_st(uint8_t*, int off, uint32_t v) { *(lds_u32_t*)(size_t)off = v; }
+__device__ __forceinline__ float lds_f32(uint32_t off) { return *(const lds_f32_t*)(size_t)off; }
+__device__ __forceinline__ f32x2_t lds_f32x2(uint32_t off) { return *(const lds_f32x2_t*)(size_t)off; }
+
+// next raw MT word from old words u = x[i], v = x[i+1] and m = x[i+397] (or the new
+// x[i-227]): m ^ (((u & UPPER) | (v & LOWER)) >> 1) ^ (v & 1 ? MATRIX_A : 0)
+// (MT19937RNGEngine.h:172-175), as 5 VALU ops: bitop3 mux, shift, 1-bit sign
+// extract, bitop3 "(s & A) ^ m", xor.
+constexpr unsigned kMux = 0xCA;     // a ? b : c, bitwise
+constexpr unsigned kAndXor = 0x6A;  // (a & b) ^ c
+__device__ __forceinline__ uint32_t mt_next(uint32_t u, uint32_t v, uint32_t m) {
+  const uint32_t y = __builtin_amdgcn_bitop3_b32(0x80000000u, u, v, kMux);
+  const uint32_t s = (uint32_t)__builtin_amdgcn_sbfe((int)v, 0, 1);
+  return __builtin_amdgcn_bitop3_b32(s, kMatrixA, m, kAndXor) ^ (y >> 1);
 }
 
 // In-place twist of the windows (MT19937RNGEngine.h:164-175).  Word i of the new block
@@ -391,7 +420,7 @@ __device__ __forceinline__ void twist_all(uint8_t* lds, const TwistPlan& P) {
   if (P.on) {
 #pragma unroll
     for (int r = 0; r < kR12; r++)
-      nv[r] = lds_u32(lds, o + 64 * r + 4 * kMtM) ^ mt_twist(lds_u32(lds, o + 64 * r), lds_u32(lds, o + 64 * r + 4));
+      nv[r] = mt_next(lds_u32(lds, o + 64 * r), lds_u32(lds, o + 64 * r + 4), lds_u32(lds, o + 64 * r + 4 * kMtM));
   }
   __syncthreads();
   if (P.on) {
@@ -406,7 +435,7 @@ __device__ __forceinline__ void twist_all(uint8_t* lds, const TwistPlan& P) {
   if (P.on) {
 #pragma unroll
     for (int r = 0; r < kR12; r++)
-      nv[r] = lds_u32(lds, o + 64 * r) ^ mt_twist(lds_u32(lds, o + 64 * r + 4 * 227), lds_u32(lds, o + 64 * r + 4 * 228));
+      nv[r] = mt_next(lds_u32(lds, o + 64 * r + 4 * 227), lds_u32(lds, o + 64 * r + 4 * 228), lds_u32(lds, o + 64 * r));
   }
   __syncthreads();
   if (P.on) {
@@ -423,7 +452,7 @@ __device__ __forceinline__ void twist_all(uint8_t* lds, const TwistPlan& P) {
     for (int r = 0; r < kR3; r++) {
       const bool last = (r == kR3 - 1) && (P.g + 16 * r == 169);
       const int ov = last ? o - 4 * P.g - 4 * 455 : o + 64 * r;  // ov + 4*455 -> x[0] of this window
-      nv[r] = lds_u32(lds, o + 64 * r + 4 * 227) ^ mt_twist(lds_u32(lds, o + 64 * r + 4 * 454), lds_u32(lds, ov + 4 * 455));
+      nv[r] = mt_next(lds_u32(lds, o + 64 * r + 4 * 454), lds_u32(lds, ov + 4 * 455), lds_u32(lds, o + 64 * r + 4 * 227));
     }
   }
   __syncthreads();
@@ -443,6 +472,22 @@ __constant__ float c_tab_bf16[3 * 256];  // R | C | S, set once from fks::tables
 constexpr int kLdsTabBytes = 256 * 4 + 256 * 8;
 constexpr int kLdsStBytes = (kMaxSeedsPerPass + 1) * kMtN * 4;
 
+// bf16 Box-Muller pair before the final rounding: (R[a] * C[b], R[a] * S[b]) + 0 as ONE
+// v_pk_fma_f32 (R*C is exact in f32: 8-bit x 8-bit significands; the +0 addend turns
+// -0 into +0 like normal_fill_16's "+ mean").  R at LDS 0, (C,S) pairs at LDS 1024.
+__device__ __forceinline__ f32x2_t z_pair_bf16_raw(uint32_t r1, uint32_t r2) {
+  const uint32_t a4 = mt_temper_u8x4(r1), b8 = mt_temper_u8x8(r2);
+#if FKS_DIAG >= 3  // diagnostics: no table lookups (wrong values)
+  const float r = __uint_as_float(a4 | 0x3f800000u);
+  const f32x2_t cs = {__uint_as_float(b8 | 0x3f000000u), __uint_as_float(b8 | 0x3e000000u)};
+#else
+  const float r = lds_f32(a4);
+  const f32x2_t cs = lds_f32x2(1024 + b8);
+#endif
+  const f32x2_t rr = {r, r}, zero = {0.0f, 0.0f};
+  return __builtin_elementwise_fma(rr, cs, zero);
+}
+
 // z pair of seed k for this lane's 16-block slot: raw words j1, j1+8 -> (z_j, z_{j+8})
 template <int DT>
 __device__ __forceinline__ void z_pair(const uint8_t* lds, uint32_t r1, uint32_t r2, float& z1, float& z2) {
@@ -451,17 +496,51 @@ __device__ __forceinline__ void z_pair(const uint8_t* lds, uint32_t r1, uint32_t
   } else {
     // normal_fill_16<BFloat16>: z = bf16(R[a] * C[b]) * 1 + 0 (std, mean).  R*C is exact
     // in f32 (8-bit x 8-bit significands) and fma(R, C, +0) turns -0 into +0 like "+ mean".
-    const uint32_t a4 = mt_temper_u8x4(r1), b4 = mt_temper_u8x4(r2);
-#if FKS_DIAG >= 3  // diagnostics: no table lookups (wrong values)
-    const float r = __uint_as_float(a4 | 0x3f800000u);
-    const float2 cs = make_float2(__uint_as_float(b4 | 0x3f000000u), __uint_as_float(b4 | 0x3e000000u));
-#else
-    const float r = *reinterpret_cast<const float*>(lds + a4);
-    const float2 cs = *reinterpret_cast<const float2*>(lds + 1024 + 2 * b4);
-#endif
-    z1 = rbf(__fmaf_rn(r, cs.x, 0.0f));
-    z2 = rbf(__fmaf_rn(r, cs.y, 0.0f));
+    const f32x2_t zz = z_pair_bf16_raw(r1, r2);
+    z1 = rbf(zz.x);
+    z2 = rbf(zz.y);
   }
+}
+
+// The update of an element PAIR (p1, p2) through one seed, zo_utils.py:49 / :52 and
+// optimizer.py:173, in packed f32 (v_pk_mul_f32 / v_pk_add_f32: both elements per
+// instruction); every op is still rounded to the parameter dtype per element, so the
+// values are those of apply_one.
+template <int DT>
+__device__ __forceinline__ f32x2_t rnd2(f32x2_t x) {
+  f32x2_t r;
+  r.x = Traits<DT>::rnd(x.x);
+  r.y = Traits<DT>::rnd(x.y);
+  return r;
+}
+
+template <int DT, int MODE>
+__device__ __forceinline__ f32x2_t apply_pair(f32x2_t p, f32x2_t z, float g, float lr, float wd, bool has_wd) {
+  if (MODE == kModeUpdate) {
+    const f32x2_t gz = rnd2<DT>(g * z);
+    const f32x2_t t2 = rnd2<DT>(gz + rnd2<DT>(wd * p));
+    f32x2_t t;
+    t.x = has_wd ? t2.x : gz.x;
+    t.y = has_wd ? t2.y : gz.y;
+    return rnd2<DT>(p - rnd2<DT>(lr * t));
+  } else if (MODE == kModePerturb) {  // lr carries f32(scaling_factor * eps)
+    return rnd2<DT>(p + rnd2<DT>(lr * z));
+  }
+  return z;
+}
+
+template <int DT>
+__device__ __forceinline__ f32x2_t z_pair2(const uint8_t* lds, uint32_t r1, uint32_t r2) {
+  f32x2_t z;
+  if constexpr (DT == FKS_BF16) {
+    z = rnd2<DT>(z_pair_bf16_raw(r1, r2));
+  } else {
+    float z1, z2;
+    z_pair<DT>(lds, r1, r2, z1, z2);
+    z.x = z1;
+    z.y = z2;
+  }
+  return z;
 }
 
 // All seeds of the pass: every state-word read of the block is issued up front
@@ -481,30 +560,33 @@ __device__ __forceinline__ void pair_all(const uint8_t* lds, int st_off, const f
     r2[k] = lds_u32(lds, st_off + k * (kMtN * 4) + 32);
 #endif
   }
-  float z1[NS], z2[NS];
+  f32x2_t z[NS];
 #pragma unroll
-  for (int k = 0; k < NS; k++) z_pair<DT>(lds, r1[k], r2[k], z1[k], z2[k]);
+  for (int k = 0; k < NS; k++) z[k] = z_pair2<DT>(lds, r1[k], r2[k]);
+  f32x2_t p = {p1, p2};
 #pragma unroll
-  for (int k = 0; k < NS; k++) {
-    p1 = apply_one<DT>(p1, z1[k], g[k], lr, wd, has_wd, MODE);
-    p2 = apply_one<DT>(p2, z2[k], g[k], lr, wd, has_wd, MODE);
-  }
+  for (int k = 0; k < NS; k++) p = apply_pair<DT, MODE>(p, z[k], g[k], lr, wd, has_wd);
+  p1 = p.x;
+  p2 = p.y;
 }
 
 // one seed (partial passes)
 template <int DT, int MODE>
 __device__ __forceinline__ void pair_one(const uint8_t* lds, int st_off, int k, float g, float lr, float wd,
                                          bool has_wd, float& p1, float& p2) {
-  float z1, z2;
-  z_pair<DT>(lds, lds_u32(lds, st_off + k * (kMtN * 4)), lds_u32(lds, st_off + k * (kMtN * 4) + 32), z1, z2);
-  p1 = apply_one<DT>(p1, z1, g, lr, wd, has_wd, MODE);
-  p2 = apply_one<DT>(p2, z2, g, lr, wd, has_wd, MODE);
+  const f32x2_t z = z_pair2<DT>(lds, lds_u32(lds, st_off + k * (kMtN * 4)), lds_u32(lds, st_off + k * (kMtN * 4) + 32));
+  f32x2_t p = {p1, p2};
+  p = apply_pair<DT, MODE>(p, z, g, lr, wd, has_wd);
+  p1 = p.x;
+  p2 = p.y;
 }
 
 template <int DT, int MODE, bool FULL>
 __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255) / 256) void fks_apply_kernel(ApplyArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
+  // the lds_* accessors address LDS by offset from 0: the dynamic block must start there
+  if ((uint32_t)(size_t)(lds_u32_t*)lds32 != 0u) __builtin_trap();
   const int tid = threadIdx.x;
   const int c = blockIdx.x;
   const int nseeds = FULL ? kMaxSeedsPerPass : a.nseeds;
@@ -740,6 +822,8 @@ __global__ __launch_bounds__(kApplyThreads) void fks_irregular_kernel(IrrArgs a)
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
   uint32_t* win = reinterpret_cast<uint32_t*>(lds + kLdsTabBytes);
+  uint32_t* cnt = win + kIrrWin * kMaxSeedsPerPass;  // per-wave counters
+  if ((uint32_t)(size_t)(lds_u32_t*)lds32 != 0u) __builtin_trap();  // z_pair reads the tables at LDS 0
   const int tid = threadIdx.x;
   const int c = blockIdx.x;
   const int nseeds = a.nseeds;
@@ -808,7 +892,15 @@ __global__ __launch_bounds__(kApplyThreads) void fks_irregular_kernel(IrrArgs a)
           default: irr_tiny_lane<FKS_F16, MODE>(win, a, T, w); break;
         }
       }
-      const int n = __syncthreads_count(mine);
+      // block-wide count of `mine` through a few dynamic-LDS words (__syncthreads_count
+      // would add static LDS and move the dynamic block off address 0)
+      const uint64_t bal = __ballot(mine);
+      if ((tid & 63) == 0) cnt[tid >> 6] = (uint32_t)__popcll(bal);
+      __syncthreads();
+      int n = 0;
+#pragma unroll
+      for (int w = 0; w < kApplyThreads / 64; w++) n += (int)cnt[w];
+      __syncthreads();
       ti += n;
       if (n < kApplyThreads) break;
     }
@@ -903,7 +995,7 @@ int launch_apply(int dtype, const ApplyArgs& a, void* stream) {
 
 template <int MODE>
 static int launch_irregular_m(const IrrArgs& a, void* stream) {
-  const size_t lds = (size_t)kLdsTabBytes + sizeof(uint32_t) * kIrrWin * (size_t)kMaxSeedsPerPass;
+  const size_t lds = (size_t)kLdsTabBytes + sizeof(uint32_t) * (kIrrWin * (size_t)kMaxSeedsPerPass + 16);
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fks_irregular_kernel<MODE>),

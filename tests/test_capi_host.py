@@ -79,21 +79,30 @@ def test_bf16_tables_reproduce_pinned_stream(golden):
     assert np.array_equal(got.reshape(-1), ref)
 
 
+def test_f16_tables_reproduce_pinned_stream(golden):
+    """z = round_f16(R[a] * C[b]) (+0) over the pinned 2^18 f16 stream (11-bit uniforms)."""
+    _, L = _lib()
+    r = np.zeros(2048, np.float32)
+    c = np.zeros(2048, np.float32)
+    s = np.zeros(2048, np.float32)
+    assert L.fks_host_tables(2, r.ctypes.data, c.ctypes.data, s.ctypes.data, 2048) == 0
+    ref = golden("normal_streams.npz")["long_float16"]
+    u = O.Generator(2024).u32(ref.size) & 0x7FF
+    blk = u.reshape(-1, 16)
+    a, b = blk[:, :8].reshape(-1), blk[:, 8:].reshape(-1)
+    zc = ((r[a] * c[b]) + np.float32(0.0)).astype(np.float16).view(np.uint16)
+    zs = ((r[a] * s[b]) + np.float32(0.0)).astype(np.float16).view(np.uint16)
+    got = np.empty((blk.shape[0], 16), np.uint16)
+    got[:, :8] = zc.reshape(-1, 8)
+    got[:, 8:] = zs.reshape(-1, 8)
+    assert np.array_equal(got.reshape(-1), ref)
+
+
 def test_tables_reject_bad_args():
     _, L = _lib()
     buf = np.zeros(16, np.float32)
     assert L.fks_host_tables(0, buf.ctypes.data, buf.ctypes.data, buf.ctypes.data, 16) < 0
     assert L.fks_last_error()
-
-
-def _consumed(shapes):
-    """Words the oracle generator consumes for sequential torch.normal calls."""
-    g = O.Generator(7)
-    for n in shapes:
-        g.normal(n, O.BF16)
-    left, nxt = g.left_next()
-    # state after k words drawn: k = 624 * twists_done - left ... recover from (left, next)
-    return g
 
 
 @pytest.mark.parametrize("shapes", [[16, 32, 624], [37, 5, 3, 16], [5, 3, 1, 7, 100], [1, 1, 1, 15, 17]])

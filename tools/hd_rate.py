@@ -1,0 +1,81 @@
+"""PCIe-inclusive reconstruct rate and K sweep.
+
+The north star's path starts and ends in host memory: model_0 arrives on the host,
+the reconstructed parameters go back to it.  This measures, for the 7B bf16 buffer:
+  * H2D of model_0 from pinned host memory, the reconstruct, D2H of the result;
+  * the device-resident reconstruct time for K in a sweep (HBM fraction vs K).
+Prints one JSON line.  Usage: python tools/hd_rate.py [--params N] [--ks 1,19,304,4096]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fate-llm_amd", "python"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def timed(fn):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--params", type=int, default=0)
+    ap.add_argument("--ks", default="1,19,304,4096")
+    ap.add_argument("--hd-k", type=int, default=4096)
+    args = ap.parse_args()
+    from fate_llm.algo.fedkseed import codec
+
+    dev = torch.device("cuda", 0)
+    shapes = [(args.params,)] if args.params else bench.llama7b_shapes()
+    total = sum(bench.numel(s) for s in shapes)
+    flat = torch.empty(total, dtype=torch.bfloat16, device=dev).normal_(0.0, 0.02)
+    views, off = [], 0
+    for s in shapes:
+        views.append(flat[off:off + bench.numel(s)])
+        off += bench.numel(s)
+    specs = [codec.ParamSpec(v, lr=1e-5, weight_decay=0.01) for v in views]
+    seeds, scalars = bench.synthetic_seeds(max(max(int(k) for k in args.ks.split(",")), args.hd_k))
+    out = {"params": total, "bytes": total * 2}
+
+    sweep = {}
+    for k in [int(x) for x in args.ks.split(",")]:
+        ks, kv = seeds[:k], [g if g != 0.0 else 1.0 for g in scalars[:k]]
+        codec.directional_step(specs, ks[:1], kv[:1])  # warm the plan caches
+        t = timed(lambda: codec.directional_step(specs, ks, kv))
+        sweep[k] = {"s": round(t, 4), "GBps": round(total * 2 / t / 1e9, 3),
+                    "hbm_frac_of_8TBps": round(2 * total * 2 * -(-k // 19) / t / 8e12, 5)}
+        print(json.dumps({"k": k, **sweep[k]}), flush=True)
+    out["k_sweep"] = sweep
+
+    host = torch.empty(total, dtype=torch.bfloat16, pin_memory=True)
+    t_d2h0 = timed(lambda: host.copy_(flat, non_blocking=True))  # host gets real values
+    t_h2d = timed(lambda: flat.copy_(host, non_blocking=True))
+    if args.hd_k in sweep:
+        t_rec = sweep[args.hd_k]["s"]
+    else:
+        ks = [s for s, g in zip(seeds[:args.hd_k], scalars[:args.hd_k]) if g != 0.0]
+        kv = [g for g in scalars[:args.hd_k] if g != 0.0]
+        t_rec = timed(lambda: codec.directional_step(specs, ks, kv))
+    t_d2h = timed(lambda: host.copy_(flat, non_blocking=True))
+    out.update({"k": args.hd_k, "h2d_s": round(t_h2d, 4), "h2d_GBps": round(total * 2 / t_h2d / 1e9, 2),
+                "reconstruct_s": round(t_rec, 3), "d2h_s": round(t_d2h, 4),
+                "d2h_GBps": round(total * 2 / t_d2h / 1e9, 2), "d2h_first_s": round(t_d2h0, 4),
+                "device_resident_GBps": round(total * 2 / t_rec / 1e9, 4),
+                "pcie_inclusive_GBps": round(total * 2 / (t_h2d + t_rec + t_d2h) / 1e9, 4)})
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
