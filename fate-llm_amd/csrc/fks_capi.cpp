@@ -310,7 +310,7 @@ struct WsSizes {
 struct WsLayout {
   size_t header = 0;  // bytes of the uploaded header
   size_t off_polys = 0, off_cb = 0, off_ipolys = 0, off_ilo = 0, off_ihi = 0, off_segs = 0, off_runs = 0,
-         off_tiny = 0, off_seeds = 0, off_g = 0, off_states = 0;
+         off_tiny = 0, off_seeds = 0, off_g = 0, off_sink = 0, off_states = 0;
   size_t total = 0;
 };
 
@@ -330,6 +330,7 @@ WsLayout ws_layout(const WsSizes& z) {
   put(w.off_seeds, sizeof(uint64_t) * k);
   put(w.off_g, sizeof(float) * 3 * k);
   w.header = o;
+  put(w.off_sink, 256);
   const size_t chunks = (size_t)std::max(z.reg_chunks, z.irr_chunks);
   put(w.off_states, sizeof(uint32_t) * kMtN * (size_t)kMaxSeedsPerPass * chunks);
   w.total = o;
@@ -490,10 +491,17 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
         aa.g = dg + (size_t)d * k + s0;
         aa.segs = reinterpret_cast<const DevSeg*>(ws + seg_off[d]);
         aa.chunk_block = ja.chunk_block;
+        aa.sink = reinterpret_cast<uint64_t*>(ws + W.off_sink);
         aa.nsegs = (int)L.segs[d].size();
         aa.nchunks = P.nchunks;
         aa.nseeds = nb;
         aa.mode = mode;
+        if (mode == kModeUpdate) {  // specialise the weight-decay select away when uniform
+          size_t nwd = 0;
+          for (const DevSeg& sg : L.segs[d]) nwd += (sg.flags & FKS_HAS_WD) ? 1 : 0;
+          if (nwd == L.segs[d].size()) aa.mode = kModeUpdateWd;
+          else if (nwd == 0) aa.mode = kModeUpdateNoWd;
+        }
         check(timed(0, stream, [&] { return launch_apply(d, aa, stream); }), "fks_apply_kernel");
       }
     }

@@ -23,6 +23,12 @@
 #ifndef FKS_DIAG
 #define FKS_DIAG 0  // diagnostic builds only (make diag): timing variants with wrong results
 #endif
+#ifndef FKS_STAGED
+#define FKS_STAGED 0  // bf16 pair phase: all indices, then all lookups, then all products
+#endif
+#ifndef FKS_UNROLL2
+#define FKS_UNROLL2 0  // apply block loop unrolled by two (slots swap roles)
+#endif
 
 namespace fks {
 namespace {
@@ -352,47 +358,17 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
 }
 
 // ------------------------------------------------------------------ apply kernel
-// In-place twist of nseeds windows (MT19937RNGEngine.h:164-175).  Word i of the new
-// block needs OLD words i and i+1 plus word i+397 (old, i < 227) or i-227 (new), so
-// the 624 words form 3 dependency phases [0,227) [227,454) [454,624); word 623 pairs
-// with the NEW word 0 (MT19937RNGEngine.h:174).  Items are dealt round-robin over
-// the 320 threads; every phase reads into registers, barriers, then writes (word i
-// reads word i+1, which another thread writes in the same phase).  Item addresses
-// depend only on (thread, nseeds), so they are computed once per kernel and the
-// three reads use immediate offsets.
-// Thread mapping: tid = 16 k + g (k < kMaxSeedsPerPass seeds, g < 16); item r of a
-// phase is word lo + g + 16 r of window k, so every LDS access of a phase is ONE
-// per-thread base address plus an immediate offset (64 r + phase constant), and the
-// 16 lanes of a seed touch 16 consecutive words (conflict-free).
-constexpr int kTwLanes = 16 * kMaxSeedsPerPass;   // threads with twist work
-constexpr int kR12 = (227 + 15) / 16;              // items per thread, phases 1-2 (last one partial)
-constexpr int kR3 = (170 + 15) / 16;               // items per thread, phase 3
-static_assert(kTwLanes <= kApplyThreads, "twist lanes exceed the workgroup");
-
-struct TwistPlan {
-  int base;     // byte offset of word g of window k
-  int dummy;    // a spare-window word: sink for the writes of items past the phase end
-  int g;
-  bool on;
-};
-
-__device__ __forceinline__ void twist_plan(TwistPlan& P, int tid, int st_base) {
-  const int k = tid >> 4;
-  P.g = tid & 15;
-  P.on = tid < kTwLanes;
-  P.base = st_base + 4 * (min(k, kMaxSeedsPerPass) * kMtN + P.g);
-  P.dummy = st_base + 4 * (kMaxSeedsPerPass * kMtN + (tid & 255));
-}
-
 // LDS accessors by byte offset.  The apply kernel's only LDS is its dynamic block,
 // which starts at LDS address 0 (no static __shared__; checked at kernel entry), so an
 // offset IS the address: immediates fold into ds_read/ds_write and no base add is
 // spent per access.
 typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+typedef __attribute__((address_space(3))) uint64_t lds_u64_t;
 typedef __attribute__((address_space(3))) float lds_f32_t;
 typedef __attribute__((address_space(3))) f32x2_t lds_f32x2_t;
-__device__ __forceinline__ uint32_t lds_u32(const uint8_t*, int off) { return *(const lds_u32_t*)(size_t)off; }
-__device__ __forceinline__ void lds_st(uint8_t*, int off, uint32_t v) { *(lds_u32_t*)(size_t)off = v; }
+__device__ __forceinline__ uint32_t lds_u32(int off) { return *(const lds_u32_t*)(size_t)off; }
+__device__ __forceinline__ uint64_t lds_u64(int off) { return *(const lds_u64_t*)(size_t)off; }
+__device__ __forceinline__ void lds_st(int off, uint32_t v) { *(lds_u32_t*)(size_t)off = v; }
 __device__ __forceinline__ float lds_f32(uint32_t off) { return *(const lds_f32_t*)(size_t)off; }
 __device__ __forceinline__ f32x2_t lds_f32x2(uint32_t off) { return *(const lds_f32x2_t*)(size_t)off; }
 
@@ -408,62 +384,80 @@ __device__ __forceinline__ uint32_t mt_next(uint32_t u, uint32_t v, uint32_t m) 
   return __builtin_amdgcn_bitop3_b32(s, kMatrixA, m, kAndXor) ^ (y >> 1);
 }
 
-// In-place twist of the windows (MT19937RNGEngine.h:164-175).  Word i of the new block
-// needs OLD words i and i+1 plus word i+397 (old, i < 227) or i-227 (new), so the 624
-// words form 3 dependency phases [0,227) [227,454) [454,624), and word 623 pairs with
-// the NEW word 0 (MT19937RNGEngine.h:174).  Each phase reads into registers, barriers,
-// then writes (word i reads word i+1, which another lane rewrites in the same phase).
-__device__ __forceinline__ void twist_all(uint8_t* lds, const TwistPlan& P) {
-  uint32_t nv[kR12];
-  const int o = P.base;
-  // phase 1: words [0, 227): m = x[i + 397] (old)
-  if (P.on) {
+// Seed windows in LDS: window k at kLdsTabBytes + 2496 k, its words PERMUTED inside each
+// 16-block so that the Box-Muller pair (j, j+8) is one aligned 8-byte word pair: one
+// conflict-free ds_read_b64 per seed and lane in the pair phase.
+__host__ __device__ constexpr int wperm(int i) { return (i & ~15) | ((i & 7) << 1) | ((i >> 3) & 1); }
+constexpr int kWinBytes = kMtN * 4;
+
+// In-place twist of the windows (MT19937RNGEngine.h:164-175), WAVE-LOCAL: wave w owns
+// windows w, w+5, w+10, w+15.  Word i of the new block needs OLD words i, i+1 and
+// i+397 (i < 227) or the NEW word i-227, so the 624 words form 3 dependency phases
+// [0,227) [227,454) [454,624); word 623 pairs with the NEW word 0.  A wave reads all
+// its items of a phase into registers before writing any, and a wave's LDS
+// operations execute in order, so no workgroup barrier is needed inside the twist.
+// Lane l handles i = lo + l + 64 j: wperm(i + 64 j) = wperm(i) + 64 j, so each phase
+// needs three per-lane byte offsets (u, v, m) and immediates for j and the window.
+constexpr int kWaves = kApplyThreads / 64;
+constexpr int kWinPerWave = (kMaxSeedsPerPass + kWaves - 1) / kWaves;
+
+struct TwistPlan {
+  int u[3], v[3], m[3];  // byte offsets in window 0 of words i, i+1, m-index for j = 0
+  int v3last;            // phase 3, j = 2: lane 41 (i = 623) pairs with the new x[0]
+  int wave;
+  int lane;
+};
+
+__device__ __forceinline__ void twist_plan(TwistPlan& P, int tid, int st_base) {
+  P.wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  P.lane = tid & 63;
+  const int lo[3] = {0, 227, 454};
 #pragma unroll
-    for (int r = 0; r < kR12; r++)
-      nv[r] = mt_next(lds_u32(lds, o + 64 * r), lds_u32(lds, o + 64 * r + 4), lds_u32(lds, o + 64 * r + 4 * kMtM));
+  for (int ph = 0; ph < 3; ph++) {
+    const int i = lo[ph] + P.lane;
+    P.u[ph] = st_base + 4 * wperm(i);
+    P.v[ph] = st_base + 4 * wperm(i + 1);
+    P.m[ph] = st_base + 4 * wperm(ph == 0 ? i + kMtM : i - (kMtN - kMtM));
   }
-  __syncthreads();
-  if (P.on) {
+  // i = 454 + 41 + 128 = 623: its next word is the new x[0]; expressed relative to j = 2
+  P.v3last = P.lane == 41 ? st_base + 4 * wperm(0) - 2 * 256 : P.v[2];
+}
+
+template <int PH>
+__device__ __forceinline__ void twist_phase(const TwistPlan& P, int nseeds) {
+  constexpr int len = PH == 2 ? kMtN - 454 : 227;
+  constexpr int nj = (len + 63) / 64;
+  uint32_t nv[kWinPerWave][nj];
 #pragma unroll
-    for (int r = 0; r < kR12; r++) {
-      const bool ok = r < kR12 - 1 || P.g + 16 * r < 227;
-      lds_st(lds, ok ? o + 64 * r : P.dummy, nv[r]);
+  for (int t = 0; t < kWinPerWave; t++) {
+    const int k = P.wave + kWaves * t;
+    if (k < nseeds) {  // wave-uniform
+#pragma unroll
+      for (int j = 0; j < nj; j++) {
+        const int w = k * kWinBytes + 256 * j;
+        const int vo = (PH == 2 && j == nj - 1) ? P.v3last : P.v[PH];
+        nv[t][j] = mt_next(lds_u32(P.u[PH] + w), lds_u32(vo + w), lds_u32(P.m[PH] + w));
+      }
     }
   }
-  __syncthreads();
-  // phase 2: words [227, 454): m = x[i - 227] (new, phase 1)
-  if (P.on) {
+  asm volatile("" ::: "memory");  // every read of the phase is issued before any write
 #pragma unroll
-    for (int r = 0; r < kR12; r++)
-      nv[r] = mt_next(lds_u32(lds, o + 64 * r + 4 * 227), lds_u32(lds, o + 64 * r + 4 * 228), lds_u32(lds, o + 64 * r));
-  }
-  __syncthreads();
-  if (P.on) {
+  for (int t = 0; t < kWinPerWave; t++) {
+    const int k = P.wave + kWaves * t;
+    if (k < nseeds) {
 #pragma unroll
-    for (int r = 0; r < kR12; r++) {
-      const bool ok = r < kR12 - 1 || P.g + 16 * r < 227;
-      lds_st(lds, ok ? o + 64 * r + 4 * 227 : P.dummy, nv[r]);
+      for (int j = 0; j < nj; j++) {
+        if (j < nj - 1 || P.lane + 64 * j < len) lds_st(P.u[PH] + k * kWinBytes + 256 * j, nv[t][j]);
+      }
     }
   }
-  __syncthreads();
-  // phase 3: words [454, 624): m = x[i - 227] (new, phase 2); word 623 pairs with new x[0]
-  if (P.on) {
-#pragma unroll
-    for (int r = 0; r < kR3; r++) {
-      const bool last = (r == kR3 - 1) && (P.g + 16 * r == 169);
-      const int ov = last ? o - 4 * P.g - 4 * 455 : o + 64 * r;  // ov + 4*455 -> x[0] of this window
-      nv[r] = mt_next(lds_u32(lds, o + 64 * r + 4 * 454), lds_u32(lds, ov + 4 * 455), lds_u32(lds, o + 64 * r + 4 * 227));
-    }
-  }
-  __syncthreads();
-  if (P.on) {
-#pragma unroll
-    for (int r = 0; r < kR3; r++) {
-      const bool ok = r < kR3 - 1 || P.g + 16 * r < 170;
-      lds_st(lds, ok ? o + 64 * r + 4 * 454 : P.dummy, nv[r]);
-    }
-  }
-  __syncthreads();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void twist_all(const TwistPlan& P, int nseeds) {
+  twist_phase<0>(P, nseeds);
+  twist_phase<1>(P, nseeds);
+  twist_phase<2>(P, nseeds);
 }
 
 __constant__ float c_tab_bf16[3 * 256];  // R | C | S, set once from fks::tables()
@@ -516,12 +510,20 @@ __device__ __forceinline__ f32x2_t rnd2(f32x2_t x) {
 
 template <int DT, int MODE>
 __device__ __forceinline__ f32x2_t apply_pair(f32x2_t p, f32x2_t z, float g, float lr, float wd, bool has_wd) {
-  if (MODE == kModeUpdate) {
+  if (MODE == kModeUpdate || MODE == kModeUpdateWd || MODE == kModeUpdateNoWd) {
     const f32x2_t gz = rnd2<DT>(g * z);
-    const f32x2_t t2 = rnd2<DT>(gz + rnd2<DT>(wd * p));
     f32x2_t t;
-    t.x = has_wd ? t2.x : gz.x;
-    t.y = has_wd ? t2.y : gz.y;
+    if (MODE == kModeUpdateNoWd) {
+      t = gz;
+    } else {
+      const f32x2_t t2 = rnd2<DT>(gz + rnd2<DT>(wd * p));
+      if (MODE == kModeUpdateWd) {
+        t = t2;
+      } else {
+        t.x = has_wd ? t2.x : gz.x;
+        t.y = has_wd ? t2.y : gz.y;
+      }
+    }
     return rnd2<DT>(p - rnd2<DT>(lr * t));
   } else if (MODE == kModePerturb) {  // lr carries f32(scaling_factor * eps)
     return rnd2<DT>(p + rnd2<DT>(lr * z));
@@ -553,16 +555,41 @@ __device__ __forceinline__ void pair_all(const uint8_t* lds, int st_off, const f
 #pragma unroll
   for (int k = 0; k < NS; k++) {
 #if FKS_DIAG == 4  // diagnostics: every lane reads the same (broadcast) words (wrong values)
-    r1[k] = lds_u32(lds, kLdsTabBytes + k * (kMtN * 4));
-    r2[k] = lds_u32(lds, kLdsTabBytes + k * (kMtN * 4) + 32);
+    const uint64_t w = lds_u64(kLdsTabBytes + k * kWinBytes);
 #else
-    r1[k] = lds_u32(lds, st_off + k * (kMtN * 4));
-    r2[k] = lds_u32(lds, st_off + k * (kMtN * 4) + 32);
+    const uint64_t w = lds_u64(st_off + k * kWinBytes);  // (word j, word j+8), permuted window
 #endif
+    r1[k] = (uint32_t)w;
+    r2[k] = (uint32_t)(w >> 32);
   }
   f32x2_t z[NS];
+  if constexpr (DT == FKS_BF16 && FKS_STAGED) {
+    // staged: every table index first, then every lookup, then the products, so the
+    // LDS latency of the lookups overlaps the other seeds' tempering
+    uint32_t ia[NS], ib[NS];
 #pragma unroll
-  for (int k = 0; k < NS; k++) z[k] = z_pair2<DT>(lds, r1[k], r2[k]);
+    for (int k = 0; k < NS; k++) {
+      ia[k] = mt_temper_u8x4(r1[k]);
+      ib[k] = mt_temper_u8x8(r2[k]);
+    }
+    asm volatile("" ::: "memory");
+    float rr[NS];
+    f32x2_t cs[NS];
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+      rr[k] = lds_f32(ia[k]);
+      cs[k] = lds_f32x2(1024 + ib[k]);
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+      const f32x2_t r2v = {rr[k], rr[k]}, zero = {0.0f, 0.0f};
+      z[k] = rnd2<DT>(__builtin_elementwise_fma(r2v, cs[k], zero));
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < NS; k++) z[k] = z_pair2<DT>(lds, r1[k], r2[k]);
+  }
   f32x2_t p = {p1, p2};
 #pragma unroll
   for (int k = 0; k < NS; k++) p = apply_pair<DT, MODE>(p, z[k], g[k], lr, wd, has_wd);
@@ -574,7 +601,8 @@ __device__ __forceinline__ void pair_all(const uint8_t* lds, int st_off, const f
 template <int DT, int MODE>
 __device__ __forceinline__ void pair_one(const uint8_t* lds, int st_off, int k, float g, float lr, float wd,
                                          bool has_wd, float& p1, float& p2) {
-  const f32x2_t z = z_pair2<DT>(lds, lds_u32(lds, st_off + k * (kMtN * 4)), lds_u32(lds, st_off + k * (kMtN * 4) + 32));
+  const uint64_t w = lds_u64(st_off + k * kWinBytes);
+  const f32x2_t z = z_pair2<DT>(lds, (uint32_t)w, (uint32_t)(w >> 32));
   f32x2_t p = {p1, p2};
   p = apply_pair<DT, MODE>(p, z, g, lr, wd, has_wd);
   p1 = p.x;
@@ -600,10 +628,9 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
       tabCS[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
     }
   }
-  uint32_t* st = reinterpret_cast<uint32_t*>(lds + kLdsTabBytes);
   for (int idx = tid; idx < nseeds * kMtN; idx += kApplyThreads) {
     const int k = idx / kMtN, i = idx - k * kMtN;
-    st[k * kMtN + i] = a.states[((size_t)k * a.nchunks + c) * kMtN + i];
+    lds_st(kLdsTabBytes + k * kWinBytes + 4 * wperm(i), a.states[((size_t)k * a.nchunks + c) * kMtN + i]);
   }
   TwistPlan plan;
   twist_plan(plan, tid, kLdsTabBytes);
@@ -618,7 +645,7 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
   // i.e. block words j1 = 16*(q/8) + q%8 and j1 + 8 (DistributionTemplates.h:141-146).
   const bool lane_on = tid < kMtN / 2;
   const int j1 = 16 * (tid >> 3) + (tid & 7);
-  const int st_off = kLdsTabBytes + 4 * j1;
+  const int st_off = kLdsTabBytes + 4 * wperm(j1);  // the (j1, j1 + 8) word pair
 
   // The lane's current segment, cached in registers; positions only grow.
   int cur;
@@ -663,36 +690,38 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
   const bool odd = (tid & 1) != 0;
   constexpr int kEs = DT == FKS_F32 ? 4 : 2;
   typedef typename Traits<DT>::Pair Pair;
-  struct Slot { uint64_t addr; float lr, wd; bool wdf, on; Pair raw; };
-  auto fetch = [&](int64_t b) {
+  struct Slot { uint64_t addr; float lr, wd; uint32_t wdf, on; Pair raw; };
+  auto fetch = [&](int64_t b) -> Slot {
     Slot sl;
     const int64_t s1 = (int64_t)kMtN * b + j1;
     while (s1 >= seg_end) { cur++; load_seg(); }
-    sl.on = lane_on && s1 >= seg_start;
+    const bool on = lane_on && s1 >= seg_start;
+    sl.on = on;
     sl.lr = seg_lr; sl.wd = seg_wd; sl.wdf = seg_wdf;
-    // off lanes read a valid dummy word, so the load is unconditional and its wait
-    // lands at first use, a block later
-    sl.addr = sl.on ? seg_ptr + (uint64_t)(s1 - seg_start + (odd ? 7 : 0)) * kEs : (uint64_t)(uintptr_t)a.states;
+    // off lanes read and write a workspace sink, so the load and the store are
+    // unconditional: the store is then always counted in vmcnt and the next wait for a
+    // prefetched pair can leave it outstanding (a maybe-executed store makes the
+    // compiler wait for it)
+    sl.addr = on ? seg_ptr + (uint64_t)(s1 - seg_start + (odd ? 7 : 0)) * kEs : (uint64_t)(uintptr_t)a.sink;
     sl.raw = 0;
     if (MODE != kModeWriteZ) sl.raw = Traits<DT>::load_pair(sl.addr);
     return sl;
   };
-  Slot nxt = fetch(b0);
-
-  for (int64_t b = b0; b < b1; b++) {
-    Slot sl = nxt;
-    if (FKS_DIAG < 2 || FKS_DIAG == 5) twist_all(lds, plan);  // the raw words of stream block b
-    if (FKS_DIAG >= 2 && FKS_DIAG != 5) __syncthreads();
-    if (b + 1 < b1) nxt = fetch(b + 1);
-    if (sl.on && FKS_DIAG != 1) {
+  // One block: twist, prefetch block b+1 (returned), Box-Muller + update chain, store.
+  auto step = [&](Slot sl, int64_t b) -> Slot {
+    __syncthreads();  // every wave is done reading block b-1's words
+    if (FKS_DIAG < 2 || FKS_DIAG == 5) twist_all(plan, nseeds);  // the raw words of stream block b
+    __syncthreads();  // every window holds block b
+    const Slot nxt = fetch(b + 1 < b1 ? b + 1 : b);  // (the last block re-reads itself, unused)
+    if (FKS_DIAG != 1) {  // every lane: off lanes compute garbage into the sink
       // even lane holds (p1, partner's p1), odd lane (partner's p2, p2)
       const uint32_t keep = odd ? Traits<DT>::hi(sl.raw) : Traits<DT>::lo(sl.raw);
       const uint32_t got = swap_adjacent(odd ? Traits<DT>::lo(sl.raw) : Traits<DT>::hi(sl.raw));
       float p1 = Traits<DT>::cvt(odd ? got : keep), p2 = Traits<DT>::cvt(odd ? keep : got);
       if constexpr (FULL) {
-        pair_all<DT, MODE, kMaxSeedsPerPass>(lds, st_off, gk, sl.lr, sl.wd, sl.wdf, p1, p2);
+        pair_all<DT, MODE, kMaxSeedsPerPass>(lds, st_off, gk, sl.lr, sl.wd, sl.wdf != 0, p1, p2);
       } else {
-        for (int k = 0; k < nseeds; k++) pair_one<DT, MODE>(lds, st_off, k, gk[k], sl.lr, sl.wd, sl.wdf, p1, p2);
+        for (int k = 0; k < nseeds; k++) pair_one<DT, MODE>(lds, st_off, k, gk[k], sl.lr, sl.wd, sl.wdf != 0, p1, p2);
       }
       const uint32_t b1v = Traits<DT>::bits(p1), b2v = Traits<DT>::bits(p2);
       const uint32_t back = swap_adjacent(odd ? b1v : b2v);  // even gets partner's p1, odd partner's p2
@@ -702,9 +731,26 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
 #endif
       Traits<DT>::store_pair(sl.addr, out);
     }
-    // no barrier here: the next twist's first barrier orders these LDS reads before
-    // its first write
+    return nxt;
+  };
+  // Unrolled by two with the slots swapping roles, so the prefetched pair is consumed
+  // in the register it was loaded into: a loop-carried copy would need the load's
+  // vmcnt wait at the latch, and with in-order counters that also waits for the
+  // store just issued.
+  Slot sa = fetch(b0);
+  // a store after the first prefetch, so the loop is entered with the same pending
+  // (load, store) shape as the back edge and the first wait can leave a store in flight
+  *reinterpret_cast<volatile uint32_t*>(a.sink + 1) = 0u;
+  int64_t b = b0;
+#if FKS_UNROLL2
+  for (; b + 1 < b1; b += 2) {
+    const Slot sb = step(sa, b);
+    sa = step(sb, b + 1);
   }
+  if (b < b1) step(sa, b);
+#else
+  for (; b < b1; b++) sa = step(sa, b);
+#endif
 }
 
 // ------------------------------------------------------------------ irregular kernel
@@ -982,13 +1028,17 @@ int launch_apply(int dtype, const ApplyArgs& a, void* stream) {
     int e = ensure_tables();
     if (e) return e;
   }
-  switch (dtype * 4 + a.mode) {
-    case FKS_F32 * 4 + kModeUpdate: return launch_apply_t<FKS_F32, kModeUpdate>(a, stream);
-    case FKS_F32 * 4 + kModePerturb: return launch_apply_t<FKS_F32, kModePerturb>(a, stream);
-    case FKS_F32 * 4 + kModeWriteZ: return launch_apply_t<FKS_F32, kModeWriteZ>(a, stream);
-    case FKS_BF16 * 4 + kModeUpdate: return launch_apply_t<FKS_BF16, kModeUpdate>(a, stream);
-    case FKS_BF16 * 4 + kModePerturb: return launch_apply_t<FKS_BF16, kModePerturb>(a, stream);
-    case FKS_BF16 * 4 + kModeWriteZ: return launch_apply_t<FKS_BF16, kModeWriteZ>(a, stream);
+  switch (dtype * 8 + a.mode) {
+    case FKS_F32 * 8 + kModeUpdate: return launch_apply_t<FKS_F32, kModeUpdate>(a, stream);
+    case FKS_F32 * 8 + kModeUpdateWd: return launch_apply_t<FKS_F32, kModeUpdateWd>(a, stream);
+    case FKS_F32 * 8 + kModeUpdateNoWd: return launch_apply_t<FKS_F32, kModeUpdateNoWd>(a, stream);
+    case FKS_F32 * 8 + kModePerturb: return launch_apply_t<FKS_F32, kModePerturb>(a, stream);
+    case FKS_F32 * 8 + kModeWriteZ: return launch_apply_t<FKS_F32, kModeWriteZ>(a, stream);
+    case FKS_BF16 * 8 + kModeUpdate: return launch_apply_t<FKS_BF16, kModeUpdate>(a, stream);
+    case FKS_BF16 * 8 + kModeUpdateWd: return launch_apply_t<FKS_BF16, kModeUpdateWd>(a, stream);
+    case FKS_BF16 * 8 + kModeUpdateNoWd: return launch_apply_t<FKS_BF16, kModeUpdateNoWd>(a, stream);
+    case FKS_BF16 * 8 + kModePerturb: return launch_apply_t<FKS_BF16, kModePerturb>(a, stream);
+    case FKS_BF16 * 8 + kModeWriteZ: return launch_apply_t<FKS_BF16, kModeWriteZ>(a, stream);
     default: return -FKS_ENOTSUP;
   }
 }

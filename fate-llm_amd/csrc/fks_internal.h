@@ -87,13 +87,16 @@ constexpr int kMaxSeedsPerPass = (160 * 1024 / kApplyWgPerCu - 3072) / 2496 - 1;
 constexpr int kJumpThreads = 1024;  // 16 waves, one chunk's jump per wave at a time
 constexpr int kJumpXLen = 19937 + 624;  // x[0..20560]: y[i + w] = x[i + w + 1], i < 19937, w < 624
 
-enum ApplyMode : int { kModeUpdate = 0, kModePerturb = 1, kModeWriteZ = 2 };
+// kModeUpdateWd / kModeUpdateNoWd: kModeUpdate specialised for a launch whose segments
+// all have / all lack the weight-decay term (fast kernel only; chosen by the host)
+enum ApplyMode : int { kModeUpdate = 0, kModePerturb = 1, kModeWriteZ = 2, kModeUpdateWd = 3, kModeUpdateNoWd = 4 };
 
 struct ApplyArgs {
   const uint32_t* states;       // [nseeds][nchunks][624] generator windows at chunk starts
   const float* g;               // [nseeds] update multiplier (mode 0); perturb scales ride in DevSeg::lr
   const DevSeg* segs;           // regular segments of this launch's dtype, sorted by start
   const int64_t* chunk_block;   // [nchunks + 1] first MT block of each chunk
+  uint64_t* sink;               // 16 bytes of workspace: loads/stores of idle lanes
   int32_t nsegs;
   int32_t nchunks;
   int32_t nseeds;

@@ -1,11 +1,18 @@
-"""One bf16 reconstruct pass (28 seeds, 64M params) for counter collection."""
-import sys, os
+"""One reconstruct of K seeds over an N-param buffer, twice, for kernel timing /
+counter collection (rocprofv3 around it).  python tools/perf_one.py [bf16|f32] [log2 N] [K]
+Defaults: bf16, N = 2^30 (chunks as long as the 7B bench's order of magnitude), K = 19."""
+import os
+import sys
+
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "fate-llm_amd", "python"))
-import torch
-from fate_llm.algo.fedkseed import codec
+import torch  # noqa: E402
+
+from fate_llm.algo.fedkseed import codec  # noqa: E402
+
 dev = torch.device("cuda", 0)
-n, k = 1 << 26, 28
-dt = torch.bfloat16 if (len(sys.argv) < 2 or sys.argv[1] == "bf16") else torch.float32
+dt = torch.float32 if (len(sys.argv) > 1 and sys.argv[1] == "f32") else torch.bfloat16
+n = 1 << (int(sys.argv[2]) if len(sys.argv) > 2 else 30)
+k = int(sys.argv[3]) if len(sys.argv) > 3 else 19
 buf = torch.empty(n, dtype=dt, device=dev).normal_(0, 0.02)
 specs = [codec.ParamSpec(buf, lr=1e-5, weight_decay=0.01)]
 g = torch.Generator().manual_seed(1)
