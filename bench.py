@@ -31,7 +31,9 @@ import torch.distributed as dist  # noqa: E402
 
 LLAMA7B_PARAMS = 6_738_415_616
 HBM_PEAK_GBS = 8000.0                 # MI355X spec (MI355X_MICROARCH.md)
-VALU_PEAK_TLANEOPS = 256 * 128 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD32 x 2.4 GHz = 78.6 T lane-op/s
+# non-packed VALU issue peak: 256 CUs x 4 SIMDs x 16 lanes x 2.4 GHz (a wave64 instruction
+# occupies its SIMD for 4 cycles) = 39.3 T lane-op/s; packed f32 ops count once here
+VALU_PEAK_TLANEOPS = 256 * 4 * 16 * 2.4e9 / 1e12
 
 
 def llama7b_shapes():
@@ -180,7 +182,8 @@ def main():
         ach = units * lane_ops / avg_apply_s / 1e12
         valu = {"bound": "valu", "achieved": round(ach, 3), "peak": VALU_PEAK_TLANEOPS, "unit": "Tlane-op/s",
                 "frac": round(ach / VALU_PEAK_TLANEOPS, 4), "lane_ops_per_unit": lane_ops,
-                "unit_def": "one seed*param update (z draw + update), lane-ops from rocprofv3 SQ_INSTS_VALU"}
+                "unit_def": "one seed*param update (z draw + update); lane-ops = rocprofv3 SQ_INSTS_VALU x 64 per "
+                            "seed*param (profiles/pmc_apply_r01.json); peak = non-packed VALU issue rate"}
     traffic = pmc.get("hbm_bytes_per_param_per_launch")
     out = {
         "metric": "GB/s param buffer reconstructed from (seed,scalar) list, device-resident",

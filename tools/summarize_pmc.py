@@ -33,6 +33,9 @@ def main(tag, params, seeds_full):
         "valu_lane_ops_per_seed_param": valu / units,
         "lds_bank_conflict_frac": sq[full]["SQ_LDS_BANK_CONFLICT"] / sq[full]["SQ_LDS_IDX_ACTIVE"],
         "wait_any_frac": sq[full]["SQ_WAIT_ANY"] / sq[full]["SQ_WAVE_CYCLES"],
+        # VALU issue occupancy: a wave64 VALU instruction holds its SIMD for 4 cycles;
+        # GRBM_GUI_ACTIVE sums the 8 XCDs; 1024 SIMDs
+        "valu_issue_busy_frac": sq[full]["SQ_INSTS_VALU"] * 4 / 1024 / (sq[full]["GRBM_GUI_ACTIVE"] / 8),
     }
     print(json.dumps(out, indent=1))
     return out
