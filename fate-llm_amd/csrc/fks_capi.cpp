@@ -41,7 +41,7 @@ inline size_t elem_size(int dtype) { return dtype == FKS_F32 ? 4 : 2; }
 // The fast kernel takes a tensor whose 16-blocks sit on 16-aligned stream words (so
 // none straddles an MT block), with no tail recompute, f32/bf16, 2-element aligned
 // (it moves adjacent element pairs); everything else goes to the irregular kernel.
-Layout make_layout(const fks_tensor* t, int nt) {
+Layout make_layout(const fks_tensor* t, int nt, const double* scales = nullptr) {
   Layout L;
   L.offset.resize((size_t)nt);
   bool cached = false;   // CPUGeneratorImpl::next_double_normal_sample
@@ -54,6 +54,8 @@ Layout make_layout(const fks_tensor* t, int nt) {
     const bool live = (x.flags & FKS_FROZEN) == 0;
     const uint64_t ptr = (uint64_t)(uintptr_t)x.data;
     const size_t es = elem_size(x.dtype);
+    // optimizer.py:173: scaling_factor * eps is a python double, cast to the fp32 opmath
+    const float ps = scales ? (float)scales[i] : 0.0f;
     if (n >= 16) {
       const bool fast = n % 16 == 0 && pos % 16 == 0 && x.dtype != FKS_F16 && ptr % (2 * es) == 0;
       if (live && fast) {
@@ -65,6 +67,7 @@ Layout make_layout(const fks_tensor* t, int nt) {
         s.wd = x.wd;
         s.flags = x.flags;
         s.dtype = x.dtype;
+        s.ps = ps;
         L.segs[x.dtype].push_back(s);
         L.seg_tensor[x.dtype].push_back(i);
       } else if (live) {
@@ -81,6 +84,7 @@ Layout make_layout(const fks_tensor* t, int nt) {
         r.wd = x.wd;
         r.flags = x.flags;
         r.dtype = x.dtype;
+        r.ps = ps;
         L.runs.push_back(r);
         L.run_tensor.push_back(i);
         if (n % 16) {
@@ -112,6 +116,7 @@ Layout make_layout(const fks_tensor* t, int nt) {
         d.wd = x.wd;
         d.flags |= x.flags & FKS_HAS_WD;
         d.dtype = x.dtype;
+        d.ps = ps;
         L.tiny.push_back(d);
         L.tiny_tensor.push_back(i);
       }
@@ -409,13 +414,7 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
   if (k < 0 || (k > 0 && (!seeds || !values))) throw Error(-FKS_EINVAL, "bad seed/value arrays");
   if (value_kind != FKS_VALUE_SCALAR && value_kind != FKS_VALUE_TENSOR)
     throw Error(-FKS_EINVAL, "bad value_kind");
-  std::vector<fks_tensor> tt;
-  if (tensor_scales) {  // perturb: the per-tensor scale rides in the lr slot (kModePerturb reads it)
-    tt.assign(t, t + nt);
-    for (int i = 0; i < nt; i++) tt[(size_t)i].lr = (float)tensor_scales[i];
-    t = tt.data();
-  }
-  Layout L = make_layout(t, nt);
+  Layout L = make_layout(t, nt, tensor_scales);
   const BlockRange br = shard_blocks(L.stream_len, shard, nshards);
   clip_segments(L, br);
   const bool have_reg = nsegs_total(L) > 0, have_irr = !L.runs.empty() || !L.tiny.empty();
@@ -655,6 +654,15 @@ int fks_perturb(const fks_tensor* t, int32_t nt, uint64_t seed, const double* sc
     if (nt > 0 && !scales) throw Error(-FKS_EINVAL, "null scales");
     const double one = 1.0;
     run(t, nt, &seed, &one, 1, FKS_VALUE_SCALAR, kModePerturb, workspace, ws_bytes, stream, scales);
+  });
+}
+
+int fks_perturb_step(const fks_tensor* t, int32_t nt, uint64_t seed, const double* scales, double value,
+                     int32_t value_kind, int32_t update, void* workspace, size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    if (nt > 0 && !scales) throw Error(-FKS_EINVAL, "null scales");
+    run(t, nt, &seed, &value, 1, value_kind, update ? kModePerturbUpdate : kModePerturb, workspace, ws_bytes, stream,
+        scales);
   });
 }
 

@@ -247,18 +247,22 @@ struct Traits<FKS_F16> {
   __device__ static float rnd(float x) { return rhf(x); }
 };
 
-// One parameter through one seed.  zo_utils.py:49 (has_wd) / :52 ; optimizer.py:173.
+// One parameter through one seed.  zo_utils.py:49 (has_wd) / :52 ; optimizer.py:173
+// (perturb: p + ps*z, ps = f32(scaling_factor * eps)).
 // Each statement is one torch op rounded to the parameter dtype (fp32 opmath).
 template <int DT>
-__device__ __forceinline__ float apply_one(float p, float z, float g, float lr, float wd, bool has_wd, int mode) {
+__device__ __forceinline__ float apply_one(float p, float z, float g, float lr, float wd, bool has_wd, int mode,
+                                           float ps) {
   using TR = Traits<DT>;
-  if (mode == kModeUpdate) {
+  if (mode == kModePerturb || mode == kModePerturbUpdate) {
+    p = TR::rnd(p + TR::rnd(ps * z));                  // param.data + scaling_factor * eps * z
+    if (mode == kModePerturb) return p;
+  }
+  if (mode == kModeUpdate || mode == kModePerturbUpdate) {
     const float gz = TR::rnd(g * z);                    // directional_derivative_value * z
     const float t2 = TR::rnd(gz + TR::rnd(wd * p));     // + weight_decay * param.data
     const float t = has_wd ? t2 : gz;                   // (select: keeps the seed loop branch-free)
     return TR::rnd(p - TR::rnd(lr * t));                // param.data - lr * (...)
-  } else if (mode == kModePerturb) {           // lr carries f32(scaling_factor * eps) here
-    return TR::rnd(p + TR::rnd(lr * z));      // param.data + scaling_factor * eps * z
   }
   return z;
 }
@@ -509,8 +513,13 @@ __device__ __forceinline__ f32x2_t rnd2(f32x2_t x) {
 }
 
 template <int DT, int MODE>
-__device__ __forceinline__ f32x2_t apply_pair(f32x2_t p, f32x2_t z, float g, float lr, float wd, bool has_wd) {
-  if (MODE == kModeUpdate || MODE == kModeUpdateWd || MODE == kModeUpdateNoWd) {
+__device__ __forceinline__ f32x2_t apply_pair(f32x2_t p, f32x2_t z, float g, float lr, float wd, bool has_wd,
+                                              float ps) {
+  if (MODE == kModePerturb || MODE == kModePerturbUpdate) {
+    p = rnd2<DT>(p + rnd2<DT>(ps * z));
+    if (MODE == kModePerturb) return p;
+  }
+  if (MODE == kModeUpdate || MODE == kModeUpdateWd || MODE == kModeUpdateNoWd || MODE == kModePerturbUpdate) {
     const f32x2_t gz = rnd2<DT>(g * z);
     f32x2_t t;
     if (MODE == kModeUpdateNoWd) {
@@ -525,8 +534,6 @@ __device__ __forceinline__ f32x2_t apply_pair(f32x2_t p, f32x2_t z, float g, flo
       }
     }
     return rnd2<DT>(p - rnd2<DT>(lr * t));
-  } else if (MODE == kModePerturb) {  // lr carries f32(scaling_factor * eps)
-    return rnd2<DT>(p + rnd2<DT>(lr * z));
   }
   return z;
 }
@@ -550,7 +557,7 @@ __device__ __forceinline__ f32x2_t z_pair2(const uint8_t* lds, uint32_t r1, uint
 // the sequential per-element update chain in seed order.
 template <int DT, int MODE, int NS>
 __device__ __forceinline__ void pair_all(const uint8_t* lds, int st_off, const float* g, float lr, float wd,
-                                         bool has_wd, float& p1, float& p2) {
+                                         bool has_wd, float ps, float& p1, float& p2) {
   uint32_t r1[NS], r2[NS];
 #pragma unroll
   for (int k = 0; k < NS; k++) {
@@ -592,7 +599,7 @@ __device__ __forceinline__ void pair_all(const uint8_t* lds, int st_off, const f
   }
   f32x2_t p = {p1, p2};
 #pragma unroll
-  for (int k = 0; k < NS; k++) p = apply_pair<DT, MODE>(p, z[k], g[k], lr, wd, has_wd);
+  for (int k = 0; k < NS; k++) p = apply_pair<DT, MODE>(p, z[k], g[k], lr, wd, has_wd, ps);
   p1 = p.x;
   p2 = p.y;
 }
@@ -600,11 +607,11 @@ __device__ __forceinline__ void pair_all(const uint8_t* lds, int st_off, const f
 // one seed (partial passes)
 template <int DT, int MODE>
 __device__ __forceinline__ void pair_one(const uint8_t* lds, int st_off, int k, float g, float lr, float wd,
-                                         bool has_wd, float& p1, float& p2) {
+                                         bool has_wd, float ps, float& p1, float& p2) {
   const uint64_t w = lds_u64(st_off + k * kWinBytes);
   const f32x2_t z = z_pair2<DT>(lds, (uint32_t)w, (uint32_t)(w >> 32));
   f32x2_t p = {p1, p2};
-  p = apply_pair<DT, MODE>(p, z, g, lr, wd, has_wd);
+  p = apply_pair<DT, MODE>(p, z, g, lr, wd, has_wd, ps);
   p1 = p.x;
   p2 = p.y;
 }
@@ -660,7 +667,7 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
   }
   int64_t seg_start = INT64_MAX, seg_end = INT64_MAX;
   uint64_t seg_ptr = 0;
-  float seg_lr = 0.0f, seg_wd = 0.0f;
+  float seg_lr = 0.0f, seg_wd = 0.0f, seg_ps = 0.0f;
   bool seg_wdf = false;
   auto load_seg = [&]() {
     if (cur < a.nsegs) {
@@ -669,6 +676,7 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
       seg_end = sg.start + sg.numel;
       seg_ptr = sg.ptr;
       seg_lr = sg.lr;
+      seg_ps = sg.ps;
       seg_wd = sg.wd;
       seg_wdf = (sg.flags & FKS_HAS_WD) != 0;
     } else {
@@ -690,14 +698,14 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
   const bool odd = (tid & 1) != 0;
   constexpr int kEs = DT == FKS_F32 ? 4 : 2;
   typedef typename Traits<DT>::Pair Pair;
-  struct Slot { uint64_t addr; float lr, wd; uint32_t wdf, on; Pair raw; };
+  struct Slot { uint64_t addr; float lr, wd, ps; uint32_t wdf, on; Pair raw; };
   auto fetch = [&](int64_t b) -> Slot {
     Slot sl;
     const int64_t s1 = (int64_t)kMtN * b + j1;
     while (s1 >= seg_end) { cur++; load_seg(); }
     const bool on = lane_on && s1 >= seg_start;
     sl.on = on;
-    sl.lr = seg_lr; sl.wd = seg_wd; sl.wdf = seg_wdf;
+    sl.lr = seg_lr; sl.wd = seg_wd; sl.ps = seg_ps; sl.wdf = seg_wdf;
     // off lanes read and write a workspace sink, so the load and the store are
     // unconditional: the store is then always counted in vmcnt and the next wait for a
     // prefetched pair can leave it outstanding (a maybe-executed store makes the
@@ -719,9 +727,10 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
       const uint32_t got = swap_adjacent(odd ? Traits<DT>::lo(sl.raw) : Traits<DT>::hi(sl.raw));
       float p1 = Traits<DT>::cvt(odd ? got : keep), p2 = Traits<DT>::cvt(odd ? keep : got);
       if constexpr (FULL) {
-        pair_all<DT, MODE, kMaxSeedsPerPass>(lds, st_off, gk, sl.lr, sl.wd, sl.wdf != 0, p1, p2);
+        pair_all<DT, MODE, kMaxSeedsPerPass>(lds, st_off, gk, sl.lr, sl.wd, sl.wdf != 0, sl.ps, p1, p2);
       } else {
-        for (int k = 0; k < nseeds; k++) pair_one<DT, MODE>(lds, st_off, k, gk[k], sl.lr, sl.wd, sl.wdf != 0, p1, p2);
+        for (int k = 0; k < nseeds; k++)
+          pair_one<DT, MODE>(lds, st_off, k, gk[k], sl.lr, sl.wd, sl.wdf != 0, sl.ps, p1, p2);
       }
       const uint32_t b1v = Traits<DT>::bits(p1), b2v = Traits<DT>::bits(p2);
       const uint32_t back = swap_adjacent(odd ? b1v : b2v);  // even gets partner's p1, odd partner's p2
@@ -831,8 +840,8 @@ __device__ __forceinline__ void irr_run_lane(const uint8_t* lds, const uint32_t*
   for (int k = 0; k < a.nseeds; k++) {
     float z1, z2;
     irr_z_pair<DT>(lds, win_word(win, k, w1), win_word(win, k, w1 + 8), z1, z2);
-    p1 = apply_one<DT>(p1, z1, g[k], R.lr, R.wd, has_wd, MODE);
-    p2 = apply_one<DT>(p2, z2, g[k], R.lr, R.wd, has_wd, MODE);
+    p1 = apply_one<DT>(p1, z1, g[k], R.lr, R.wd, has_wd, MODE, R.ps);
+    p2 = apply_one<DT>(p2, z2, g[k], R.lr, R.wd, has_wd, MODE, R.ps);
   }
   if (on1) TR::store(R.ptr, e1, p1);
   if (on2) TR::store(R.ptr, e1 + 8, p2);
@@ -858,7 +867,7 @@ __device__ __forceinline__ void irr_tiny_lane(const uint32_t* win, const IrrArgs
     const double v = (sin_half ? r * sin(theta) : r * cos(theta)) * 1.0 + 0.0;
     const float zf = (float)v;  // static_cast<scalar_t>(double): via float for bf16 / f16
     const float z = DT == FKS_F32 ? zf : TR::rnd(zf);
-    p = apply_one<DT>(p, z, g[k], T.lr, T.wd, has_wd, MODE);
+    p = apply_one<DT>(p, z, g[k], T.lr, T.wd, has_wd, MODE, T.ps);
   }
   TR::store(T.ptr, 0, p);
 }
@@ -1033,11 +1042,13 @@ int launch_apply(int dtype, const ApplyArgs& a, void* stream) {
     case FKS_F32 * 8 + kModeUpdateWd: return launch_apply_t<FKS_F32, kModeUpdateWd>(a, stream);
     case FKS_F32 * 8 + kModeUpdateNoWd: return launch_apply_t<FKS_F32, kModeUpdateNoWd>(a, stream);
     case FKS_F32 * 8 + kModePerturb: return launch_apply_t<FKS_F32, kModePerturb>(a, stream);
+    case FKS_F32 * 8 + kModePerturbUpdate: return launch_apply_t<FKS_F32, kModePerturbUpdate>(a, stream);
     case FKS_F32 * 8 + kModeWriteZ: return launch_apply_t<FKS_F32, kModeWriteZ>(a, stream);
     case FKS_BF16 * 8 + kModeUpdate: return launch_apply_t<FKS_BF16, kModeUpdate>(a, stream);
     case FKS_BF16 * 8 + kModeUpdateWd: return launch_apply_t<FKS_BF16, kModeUpdateWd>(a, stream);
     case FKS_BF16 * 8 + kModeUpdateNoWd: return launch_apply_t<FKS_BF16, kModeUpdateNoWd>(a, stream);
     case FKS_BF16 * 8 + kModePerturb: return launch_apply_t<FKS_BF16, kModePerturb>(a, stream);
+    case FKS_BF16 * 8 + kModePerturbUpdate: return launch_apply_t<FKS_BF16, kModePerturbUpdate>(a, stream);
     case FKS_BF16 * 8 + kModeWriteZ: return launch_apply_t<FKS_BF16, kModeWriteZ>(a, stream);
     default: return -FKS_ENOTSUP;
   }
@@ -1065,6 +1076,7 @@ int launch_irregular(const IrrArgs& a, void* stream) {
   switch (a.mode) {
     case kModeUpdate: return launch_irregular_m<kModeUpdate>(a, stream);
     case kModePerturb: return launch_irregular_m<kModePerturb>(a, stream);
+    case kModePerturbUpdate: return launch_irregular_m<kModePerturbUpdate>(a, stream);
     case kModeWriteZ: return launch_irregular_m<kModeWriteZ>(a, stream);
     default: return -FKS_ENOTSUP;
   }

@@ -49,8 +49,10 @@ struct DevSeg {
   float wd;
   uint32_t flags;  // FKS_HAS_WD
   int32_t dtype;
+  float ps;        // perturbation scale f32(scaling_factor * eps) (perturb modes)
+  uint32_t pad;
 };
-static_assert(sizeof(DevSeg) == 40, "DevSeg layout");
+static_assert(sizeof(DevSeg) == 48, "DevSeg layout");
 
 // Irregular work (fks_irregular_kernel): a run of whole 16-blocks at any stream phase ...
 struct DevRun {
@@ -62,8 +64,10 @@ struct DevRun {
   float wd;
   uint32_t flags;  // FKS_HAS_WD
   int32_t dtype;
+  float ps;        // perturbation scale (perturb modes)
+  uint32_t pad;
 };
-static_assert(sizeof(DevRun) == 48, "DevRun layout");
+static_assert(sizeof(DevRun) == 56, "DevRun layout");
 
 // ... and one element of a numel < 16 tensor (serial normal_distribution<double>)
 constexpr uint32_t kTinySin = 1u << 8;  // the element takes the pair's cached r*sin value
@@ -74,8 +78,10 @@ struct DevTiny {
   float wd;
   uint32_t flags;  // FKS_HAS_WD | kTinySin
   int32_t dtype;
+  float ps;        // perturbation scale (perturb modes)
+  uint32_t pad;
 };
-static_assert(sizeof(DevTiny) == 32, "DevTiny layout");
+static_assert(sizeof(DevTiny) == 40, "DevTiny layout");
 
 constexpr int kApplyThreads = 320;  // 312 Box-Muller pairs per 624-word block + 8 idle lanes
 #ifndef FKS_APPLY_WG_PER_CU
@@ -89,7 +95,11 @@ constexpr int kJumpXLen = 19937 + 624;  // x[0..20560]: y[i + w] = x[i + w + 1],
 
 // kModeUpdateWd / kModeUpdateNoWd: kModeUpdate specialised for a launch whose segments
 // all have / all lack the weight-decay term (fast kernel only; chosen by the host)
-enum ApplyMode : int { kModeUpdate = 0, kModePerturb = 1, kModeWriteZ = 2, kModeUpdateWd = 3, kModeUpdateNoWd = 4 };
+// kModePerturbUpdate: p + ps*z, then the update with the same z (the restore
+// perturbation of zeroth_order_step fused with its directional step)
+enum ApplyMode : int {
+  kModeUpdate = 0, kModePerturb = 1, kModeWriteZ = 2, kModeUpdateWd = 3, kModeUpdateNoWd = 4, kModePerturbUpdate = 5
+};
 
 struct ApplyArgs {
   const uint32_t* states;       // [nseeds][nchunks][624] generator windows at chunk starts

@@ -156,6 +156,30 @@ def perturb(tensors: Sequence[torch.Tensor], seed: int, scales) -> None:
         b.finish()
 
 
+def perturb_step(specs: Sequence[ParamSpec], seed: int, scales: Sequence[float], value: float,
+                 value_is_tensor: bool = True, update: bool = True) -> None:
+    """zeroth_order_step's restore perturbation fused with its directional step, in one
+    device pass: p <- p + scale_i*z, then (``update``) p <- p - lr*(value*z + wd*p) with
+    the same z.  Equal, bit for bit, to ``perturb`` followed by ``directional_step``
+    over the same tensor list."""
+    specs = list(specs)
+    if not specs:
+        return
+    if len(scales) != len(specs):
+        raise ValueError("one scale per tensor")
+    b = _Batch(specs)
+    if b.device is None:
+        return
+    L = N.load()
+    sc = np.ascontiguousarray([float(x) for x in scales], dtype=np.float64)
+    with torch.cuda.device(b.device):
+        ws, nbytes = b.workspace(1)
+        N.check(L.fks_perturb_step(ctypes.addressof(b.arr), b.n, _seed_u64(seed), sc.ctypes.data, float(value),
+                                   N.VALUE_TENSOR if value_is_tensor else N.VALUE_SCALAR, 1 if update else 0,
+                                   ws.data_ptr(), nbytes, _stream_handle(b.device)))
+        b.finish()
+
+
 def normal_(tensors: Sequence[torch.Tensor], seed: int, frozen: Optional[Sequence[bool]] = None) -> None:
     """Overwrite every tensor with the z the reference draws for it after manual_seed(seed)."""
     specs = [ParamSpec(t, frozen=bool(frozen[i]) if frozen else False) for i, t in enumerate(tensors)]

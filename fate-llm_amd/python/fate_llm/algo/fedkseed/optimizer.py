@@ -62,21 +62,36 @@ class ZerothOrderOptimizer(RandomWalkOptimizer):
     ) -> Tuple[torch.FloatTensor, torch.FloatTensor, torch.FloatTensor]:
         """x+eps*z -> loss_right; x-eps*z -> loss_left; back to x; then the update with
         g = (loss_right - loss_left) / (2 eps).  Returns (g, loss_right, loss_left); a NaN
-        loss short-circuits before the update, as in the reference."""
+        loss short-circuits before the update, as in the reference (optimizer.py:108-150).
+
+        The restore perturbation and the update use the same z, so when they walk the
+        same tensors (every grouped parameter requires grad) they run as ONE device pass
+        (codec.perturb_step); the values are those of the two separate steps."""
         self.random_perturb_parameters(directional_derivative_seed, scaling_factor=1.0)
         loss_right = closure()
         self.random_perturb_parameters(directional_derivative_seed, scaling_factor=-2.0)
         loss_left = closure()
-        self.random_perturb_parameters(directional_derivative_seed, scaling_factor=1.0)
 
-        if torch.isnan(loss_right):
-            return loss_right, loss_right, loss_left
-        if torch.isnan(loss_left):
-            return loss_left, loss_right, loss_left
+        right_nan, left_nan = bool(torch.isnan(loss_right)), bool(torch.isnan(loss_left))
+        if right_nan or left_nan:
+            self.random_perturb_parameters(directional_derivative_seed, scaling_factor=1.0)
+            return (loss_right if right_nan else loss_left), loss_right, loss_left
 
         g = (loss_right - loss_left) / (2 * self.eps)
-        g = self.directional_derivative_step(directional_derivative_seed, g)
+        clipped = self.grad_clip > 0.0 and abs(g) > self.grad_clip
+        if clipped or not self._fusable():
+            self.random_perturb_parameters(directional_derivative_seed, scaling_factor=1.0)
+            g = self.directional_derivative_step(directional_derivative_seed, g)
+            return g, loss_right, loss_left
+        torch.manual_seed(directional_derivative_seed)
+        specs = codec.resolve_groups(self.param_groups)
+        scales = [1.0 * group["eps"] for group in self.param_groups for _ in group["params"]]
+        codec.perturb_step(specs, directional_derivative_seed, scales, float(g), value_is_tensor=True, update=True)
         return g, loss_right, loss_left
+
+    def _fusable(self) -> bool:
+        """restore and update walk the same tensors: no frozen parameter in the groups"""
+        return all(p.requires_grad for group in self.param_groups for p in group["params"])
 
     def random_perturb_parameters(self, directional_derivative_seed: int, scaling_factor: float):
         """p <- p + scaling_factor*eps*z for every parameter that requires grad; frozen

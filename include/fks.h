@@ -121,6 +121,16 @@ int fks_profile_end(double* apply_ms, int64_t* n_apply, double* jump_ms, int64_t
 int fks_perturb(const fks_tensor* t, int32_t nt, uint64_t seed, const double* scales, void* workspace,
                 size_t ws_bytes, void* stream);
 
+/* The restore perturbation of zeroth_order_step fused with its directional step
+ * (optimizer.py:136 then :147 -> :92 -> zo_utils.py:49): torch.manual_seed(seed); for
+ * every tensor i: p = p + scales[i]*z, and, if `update` is nonzero, then with the SAME z
+ * p = p - lr*(g*z + wd*p) (or p - lr*g*z without FKS_HAS_WD), g = `value` of
+ * `value_kind`.  One pass instead of two; bit-identical to fks_perturb followed by
+ * fks_directional_step when both would walk the same tensor list (no frozen tensor in
+ * the optimizer's groups). */
+int fks_perturb_step(const fks_tensor* t, int32_t nt, uint64_t seed, const double* scales, double value,
+                     int32_t value_kind, int32_t update, void* workspace, size_t ws_bytes, void* stream);
+
 /* torch.manual_seed(seed); for every tensor in order: p = torch.normal(0, 1, size, dtype). */
 int fks_normal(const fks_tensor* t, int32_t nt, uint64_t seed, void* workspace, size_t ws_bytes, void* stream);
 

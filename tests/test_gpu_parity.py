@@ -312,6 +312,57 @@ def test_element_shards_equal_whole(nshards):
         assert_bitwise(to_np(t), w, "bfloat16", f"tensor {i}")
 
 
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16", "float16"])
+def test_fused_restore_and_step_vs_oracle(dtype):
+    """codec.perturb_step (restore perturbation + directional step in one pass) equals
+    the reference's two separate steps, on regular and irregular tensors, with a
+    0-dim-tensor g (rounded to the parameter dtype first)."""
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    shapes = [4800, 48, 7, 185, 6912, 3, 37, 144]
+    arrays = rand_params(shapes, dtype, seed=12)
+    ts = [from_np(a, dtype, dev) for a in arrays]
+    lrs = [1e-3] * len(shapes)
+    wds = [0.0 if i % 2 else 0.01 for i in range(len(shapes))]
+    specs = [codec.ParamSpec(t, lr=lr, weight_decay=wd) for t, lr, wd in zip(ts, lrs, wds)]
+    eps, seed = 5e-4, 24681357
+    g = float(np.float32(0.125) / np.float32(2 * eps))
+    codec.perturb_step(specs, seed, [eps] * len(ts), g, value_is_tensor=True, update=True)
+    torch.cuda.synchronize()
+    O.perturb_params(arrays, [DTC[dtype]] * len(arrays), seed, eps)
+    gg = float(torch.tensor(g, dtype=torch.float32).to(TD[dtype]).float())
+    O.reconstruct(arrays, [DTC[dtype]] * len(arrays), lrs, wds, [seed], [gg])
+    for i, (t, a) in enumerate(zip(ts, arrays)):
+        assert_bitwise(to_np(t), a, dtype, f"tensor {i}")
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_zeroth_order_step_fused_equals_unfused(dtype):
+    """ZerothOrderOptimizer.zeroth_order_step takes the fused path when every grouped
+    parameter requires grad; the result equals the reference sequence (perturb +1, -2,
+    +1 with the oracle, then the update)."""
+    from fate_llm.algo.fedkseed.optimizer import ZerothOrderOptimizer
+    dev = _dev()
+    shapes = [4800, 48, 48, 6912, 144, 7, 37]
+    arrays = rand_params(shapes, dtype, seed=13)
+    params = [torch.nn.Parameter(from_np(a, dtype, dev)) for a in arrays]
+    groups = [{"params": params[:3], "weight_decay": 0.0}, {"params": params[3:], "weight_decay": 0.01}]
+    opt = ZerothOrderOptimizer(groups, lr=1e-3, eps=5e-4, weight_decay=0.01, grad_clip=-100.0)
+    assert opt._fusable()
+    losses = iter([torch.tensor(2.5), torch.tensor(2.375)])
+    g, _, _ = opt.zeroth_order_step(777, lambda: next(losses))
+    torch.cuda.synchronize()
+    for sf in (1.0, -2.0, 1.0):
+        O.perturb_params(arrays, [DTC[dtype]] * len(arrays), 777, sf * 5e-4)
+    gv = float(g)
+    if dtype == "bfloat16":
+        gv = float(torch.tensor(gv, dtype=torch.float32).to(torch.bfloat16).float())
+    # sticky: group 0's wd (0.0) and the optimizer lr stick for every tensor
+    O.reconstruct(arrays, [DTC[dtype]] * len(arrays), [1e-3] * len(arrays), [0.0] * len(arrays), [777], [gv])
+    for i, (p, a) in enumerate(zip(params, arrays)):
+        assert_bitwise(to_np(p.data), a, dtype, f"tensor {i}")
+
+
 def test_cpu_tensors_rejected():
     from fate_llm.algo.fedkseed import codec
     _dev()
