@@ -281,6 +281,48 @@ constexpr int kJumpLdsWords = kJumpXOff + kJumpXLen + 64;  // + over-read slack 
 
 __device__ __forceinline__ uint4 lds_b128(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
 
+// acc[j] ^= c0 * w[j] ^ c1 * w[j + 1] (j < 12) for the wave-uniform coefficient pair
+// two = c0 | c1 << 1.  Scalar branches skip a clear pair and pick the one-word or the
+// 3-input-xor body (v_bitop3), so a random polynomial costs 0.75 VALU ops per word and
+// coefficient pair instead of 2.  Inline asm: compiled from C the three bodies write
+// fresh registers and every merge copies the 12 accumulators back (v_mov x 12).
+__device__ __forceinline__ void jump_pair_step(uint32_t (&acc)[12], uint32_t w0, uint32_t w1, uint32_t w2,
+                                               uint32_t w3, uint32_t w4, uint32_t w5, uint32_t w6, uint32_t w7,
+                                               uint32_t w8, uint32_t w9, uint32_t w10, uint32_t w11, uint32_t w12,
+                                               uint32_t two) {
+  asm volatile(
+      "s_cmp_eq_u32 %[two], 0\n\t"
+      "s_cbranch_scc1 .Ljend%=\n\t"
+      "s_cmp_eq_u32 %[two], 3\n\t"
+      "s_cbranch_scc1 .Ljboth%=\n\t"
+      "s_cmp_eq_u32 %[two], 1\n\t"
+      "s_cbranch_scc1 .Ljone%=\n\t"
+      "v_xor_b32 %0, %0, %[w1]\n\tv_xor_b32 %1, %1, %[w2]\n\tv_xor_b32 %2, %2, %[w3]\n\t"
+      "v_xor_b32 %3, %3, %[w4]\n\tv_xor_b32 %4, %4, %[w5]\n\tv_xor_b32 %5, %5, %[w6]\n\t"
+      "v_xor_b32 %6, %6, %[w7]\n\tv_xor_b32 %7, %7, %[w8]\n\tv_xor_b32 %8, %8, %[w9]\n\t"
+      "v_xor_b32 %9, %9, %[w10]\n\tv_xor_b32 %10, %10, %[w11]\n\tv_xor_b32 %11, %11, %[w12]\n\t"
+      "s_branch .Ljend%=\n"
+      ".Ljone%=:\n\t"
+      "v_xor_b32 %0, %0, %[w0]\n\tv_xor_b32 %1, %1, %[w1]\n\tv_xor_b32 %2, %2, %[w2]\n\t"
+      "v_xor_b32 %3, %3, %[w3]\n\tv_xor_b32 %4, %4, %[w4]\n\tv_xor_b32 %5, %5, %[w5]\n\t"
+      "v_xor_b32 %6, %6, %[w6]\n\tv_xor_b32 %7, %7, %[w7]\n\tv_xor_b32 %8, %8, %[w8]\n\t"
+      "v_xor_b32 %9, %9, %[w9]\n\tv_xor_b32 %10, %10, %[w10]\n\tv_xor_b32 %11, %11, %[w11]\n\t"
+      "s_branch .Ljend%=\n"
+      ".Ljboth%=:\n\t"
+      "v_bitop3_b32 %0, %0, %[w0], %[w1] bitop3:0x96\n\tv_bitop3_b32 %1, %1, %[w1], %[w2] bitop3:0x96\n\t"
+      "v_bitop3_b32 %2, %2, %[w2], %[w3] bitop3:0x96\n\tv_bitop3_b32 %3, %3, %[w3], %[w4] bitop3:0x96\n\t"
+      "v_bitop3_b32 %4, %4, %[w4], %[w5] bitop3:0x96\n\tv_bitop3_b32 %5, %5, %[w5], %[w6] bitop3:0x96\n\t"
+      "v_bitop3_b32 %6, %6, %[w6], %[w7] bitop3:0x96\n\tv_bitop3_b32 %7, %7, %[w7], %[w8] bitop3:0x96\n\t"
+      "v_bitop3_b32 %8, %8, %[w8], %[w9] bitop3:0x96\n\tv_bitop3_b32 %9, %9, %[w9], %[w10] bitop3:0x96\n\t"
+      "v_bitop3_b32 %10, %10, %[w10], %[w11] bitop3:0x96\n\tv_bitop3_b32 %11, %11, %[w11], %[w12] bitop3:0x96\n"
+      ".Ljend%=:"
+      : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]),
+        "+v"(acc[7]), "+v"(acc[8]), "+v"(acc[9]), "+v"(acc[10]), "+v"(acc[11])
+      : [w0] "v"(w0), [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4), [w5] "v"(w5), [w6] "v"(w6),
+        [w7] "v"(w7), [w8] "v"(w8), [w9] "v"(w9), [w10] "v"(w10), [w11] "v"(w11), [w12] "v"(w12), [two] "s"(two)
+      : "scc");
+}
+
 __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_j[];
   uint32_t* xs = lds_j + kJumpXOff;
@@ -341,11 +383,17 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
             const int rot = (4 * q) & 15;
             const uint32_t word = q < 8 ? lo : hi;
 #pragma unroll
-            for (int d = 0; d < 4; d++) {
-              // all-ones if coefficient 64 wd + 4q + d is set (scalar bit-field extract)
-              const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)word, (4 * q + d) & 31, 1);
-#pragma unroll
-              for (int j = 0; j < 12; j++) acc[j] = __builtin_amdgcn_bitop3_b32(acc[j], win[(rot + j + d) & 15], m, kXorAnd);
+            for (int d = 0; d < 4; d += 2) {
+              // coefficients 64 wd + 4q + d, +1 as a wave-uniform 2-bit code: a scalar
+              // branch skips clear coefficients, and a set pair costs ONE 3-input xor
+              // per word (v_bitop3), so a random polynomial costs 0.75 instead of 2
+              // VALU ops per word and coefficient pair
+              const uint32_t two = (word >> ((4 * q + d) & 31)) & 3u;
+              jump_pair_step(acc, win[(rot + d) & 15], win[(rot + d + 1) & 15], win[(rot + d + 2) & 15],
+                             win[(rot + d + 3) & 15], win[(rot + d + 4) & 15], win[(rot + d + 5) & 15],
+                             win[(rot + d + 6) & 15], win[(rot + d + 7) & 15], win[(rot + d + 8) & 15],
+                             win[(rot + d + 9) & 15], win[(rot + d + 10) & 15], win[(rot + d + 11) & 15],
+                             win[(rot + d + 12) & 15], two);
             }
             win[(rot + 0) & 15] = nx.x;
             win[(rot + 1) & 15] = nx.y;
