@@ -12,6 +12,12 @@ equal runs of MT19937 blocks and rank r reconstructs run r (element sharding: ev
 element still sees every seed in order, so the result is bit-identical to N = 1 and
 no collective touches the data path).  Total work is fixed: "scaling": "strong".
 
+--mode seed-shard runs the north star's C3 variant instead: rank r takes a contiguous
+1/N of the seeds, accumulates its f32 delta over the whole buffer (fks_delta_accumulate),
+one RCCL all-reduce sums the deltas over xGMI, every rank applies p = a^K p_0 - delta.
+Not the reference's rounding (DESIGN.md §7 gives its measured deviation); the default
+(--mode sequential) is the bit-exact path.
+
 Rank 0 prints ONE JSON line: the metric, the dominant kernel's roofline (HBM, as the
 north star asks, plus the VALU roofline that actually binds), and the reference CPU
 path timed on this host in the same run (cpu_baseline).
@@ -113,6 +119,7 @@ def main():
     ap.add_argument("--params", type=int, default=0, help="override: flat buffer of this many params (dev only)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", choices=("sequential", "seed-shard"), default="sequential")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -140,9 +147,17 @@ def main():
     seeds, scalars = synthetic_seeds(args.k)
     keep = [(s, g) for s, g in zip(seeds, scalars) if g != 0.0]
     ks, kv = [s for s, _ in keep], [g for _, g in keep]
+    seed_shard = args.mode == "seed-shard"
+    if seed_shard:
+        from fate_llm.algo.fedkseed import zo_utils
+        groups = [{"params": views, "lr": 1e-5, "weight_decay": 0.01}]
+        delta = torch.empty(total, dtype=torch.float32, device=dev)
 
     def step():
-        codec.directional_step(specs, ks, kv, shard=rank, nshards=world)
+        if seed_shard:
+            zo_utils.reconstruct_seed_sharded_(groups, ks, kv, lr=1e-5, weight_decay=0.01, delta=delta)
+        else:
+            codec.directional_step(specs, ks, kv, shard=rank, nshards=world)
 
     for _ in range(args.warmup):
         step()
@@ -168,11 +183,13 @@ def main():
     value = buf_bytes / (dt / args.steps) / 1e9
 
     # roofline of the dominant kernel (fks_apply_kernel), per launch, this rank
-    rank_params = total / world
+    rank_params = total if seed_shard else total / world
     n_apply = max(prof.n_apply, 1)
     avg_apply_s = prof.apply_ms / n_apply / 1e3
-    seeds_per_launch = len(ks) * args.steps / n_apply
-    alg_bytes = 2 * rank_params * 2                      # read + write the (shard of the) buffer once
+    rank_seeds = len(ks) * (rank + 1) // world - len(ks) * rank // world if seed_shard else len(ks)
+    seeds_per_launch = rank_seeds * args.steps / n_apply
+    # read + write the (shard of the) buffer once: bf16 parameters, or the f32 delta
+    alg_bytes = 2 * rank_params * (4 if seed_shard else 2)
     hbm_achieved = alg_bytes / avg_apply_s / 1e9
     pmc = load_pmc_summary()
     lane_ops = pmc.get("valu_lane_ops_per_seed_param")
@@ -184,16 +201,21 @@ def main():
                 "frac": round(ach / VALU_PEAK_TLANEOPS, 4), "lane_ops_per_unit": lane_ops,
                 "unit_def": "one seed*param update (z draw + update); lane-ops = rocprofv3 SQ_INSTS_VALU x 64 per "
                             "seed*param (profiles/pmc_apply_r01.json); peak = non-packed VALU issue rate"}
-    traffic = pmc.get("hbm_bytes_per_param_per_launch")
+    traffic = None if seed_shard else pmc.get("hbm_bytes_per_param_per_launch")
+    if seed_shard:
+        valu = None  # the committed PMC summary is the sequential kernel's
     out = {
         "metric": "GB/s param buffer reconstructed from (seed,scalar) list, device-resident",
         "value": round(value, 4), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 2), "higher_is_better": True, "scaling": "strong",
+        "mode": args.mode,
         "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random-init LLaMA-7B shapes, seeded seeds/scalars)",
-        "config": {"workload": "1xMI355X: 7B-param bf16 buffer, K=4096 seeds" if world == 1 else
+        "config": {"workload": (f"{world}xMI355X: same 7B / K={args.k}, seeds sharded {len(ks) // world}/GPU, "
+                                f"RCCL all-reduce of delta over xGMI") if seed_shard else
+                   "1xMI355X: 7B-param bf16 buffer, K=4096 seeds" if world == 1 else
                    f"{world}xMI355X: 7B-param bf16 buffer, K=4096 seeds, element-sharded",
                    "params": total, "k": args.k, "k_nonzero": len(ks), "tensors": len(shapes),
-                   "parallelism": f"element-shard{world}"},
+                   "parallelism": f"seed-shard{world}" if seed_shard else f"element-shard{world}"},
         "roofline": {"bound": "hbm", "achieved": round(hbm_achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(hbm_achieved / HBM_PEAK_GBS, 6),
                      "traffic": (round(traffic * rank_params) if traffic else None),

@@ -34,16 +34,24 @@ struct Layout {
   std::vector<DevTiny> tiny;    // single elements of numel < 16 tensors, sorted by word
   // host-only: the tensor index of every segment / run / element (fks_shard_census)
   std::vector<int> seg_tensor[3], run_tensor, tiny_tensor;
+  // seed-sharded variant (fks_delta_accumulate): the descriptors address the f32 delta
+  // buffer (element e of tensor i at delta[cum_numel(i) + e]) instead of the parameters;
+  // the dtype still selects the z generator
+  bool delta = false;
 };
 
 inline size_t elem_size(int dtype) { return dtype == FKS_F32 ? 4 : 2; }
+// bytes per element of what the kernels load and store
+inline size_t stor_size(const Layout& L, int dtype) { return L.delta ? 4 : elem_size(dtype); }
 
 // The fast kernel takes a tensor whose 16-blocks sit on 16-aligned stream words (so
 // none straddles an MT block), with no tail recompute, f32/bf16, 2-element aligned
 // (it moves adjacent element pairs); everything else goes to the irregular kernel.
-Layout make_layout(const fks_tensor* t, int nt, const double* scales = nullptr) {
+Layout make_layout(const fks_tensor* t, int nt, const double* scales = nullptr, uint64_t delta_base = 0) {
   Layout L;
+  L.delta = delta_base != 0;
   L.offset.resize((size_t)nt);
+  int64_t cum = 0;  // concatenated element offset (delta layout)
   bool cached = false;   // CPUGeneratorImpl::next_double_normal_sample
   int64_t cached_pair = 0;
   int64_t pos = 0;
@@ -52,8 +60,9 @@ Layout make_layout(const fks_tensor* t, int nt, const double* scales = nullptr) 
     L.offset[(size_t)i] = pos;
     const int64_t n = x.numel;
     const bool live = (x.flags & FKS_FROZEN) == 0;
-    const uint64_t ptr = (uint64_t)(uintptr_t)x.data;
-    const size_t es = elem_size(x.dtype);
+    const uint64_t ptr = L.delta ? delta_base + 4 * (uint64_t)cum : (uint64_t)(uintptr_t)x.data;
+    const size_t es = stor_size(L, x.dtype);
+    cum += n;
     // optimizer.py:173: scaling_factor * eps is a python double, cast to the fp32 opmath
     const float ps = scales ? (float)scales[i] : 0.0f;
     if (n >= 16) {
@@ -205,7 +214,7 @@ void clip_segments(Layout& L, BlockRange r) {
       const int64_t a = std::max(s.start, lo), b = std::min(s.start + s.numel, hi);
       if (a >= b) continue;
       DevSeg c = s;
-      c.ptr = s.ptr + (uint64_t)(a - s.start) * elem_size(s.dtype);
+      c.ptr = s.ptr + (uint64_t)(a - s.start) * stor_size(L, s.dtype);
       c.start = a;
       c.numel = b - a;
       out.push_back(c);
@@ -229,7 +238,7 @@ void clip_segments(Layout& L, BlockRange r) {
     DevRun c = R;
     c.start = R.start + 16 * i0;
     c.numel = 16 * (i1 - i0);
-    c.ptr = R.ptr + (uint64_t)(16 * i0) * elem_size(R.dtype);
+    c.ptr = R.ptr + (uint64_t)(16 * i0) * stor_size(L, R.dtype);
     c.limit = R.limit - 16 * i0;
     runs.push_back(c);
     runs_t.push_back(L.run_tensor[j]);
@@ -408,13 +417,13 @@ int timed(int which, void* stream, F&& launch) {
 
 void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* values, int k, int value_kind, int mode,
          void* workspace, size_t ws_bytes, void* stream, const double* tensor_scales = nullptr, int shard = 0,
-         int nshards = 1) {
+         int nshards = 1, uint64_t delta_base = 0) {
   validate(t, nt);
   if (nshards < 1 || shard < 0 || shard >= nshards) throw Error(-FKS_EINVAL, "bad shard");
   if (k < 0 || (k > 0 && (!seeds || !values))) throw Error(-FKS_EINVAL, "bad seed/value arrays");
   if (value_kind != FKS_VALUE_SCALAR && value_kind != FKS_VALUE_TENSOR)
     throw Error(-FKS_EINVAL, "bad value_kind");
-  Layout L = make_layout(t, nt, tensor_scales);
+  Layout L = make_layout(t, nt, tensor_scales, delta_base);
   const BlockRange br = shard_blocks(L.stream_len, shard, nshards);
   clip_segments(L, br);
   const bool have_reg = nsegs_total(L) > 0, have_irr = !L.runs.empty() || !L.tiny.empty();
@@ -549,6 +558,8 @@ int guarded(F&& f) {
   }
 }
 
+size_t workspace_total(const fks_tensor* t, int nt, int k, uint64_t delta_base);
+
 }  // namespace
 }  // namespace fks
 
@@ -560,7 +571,70 @@ int fks_workspace_size(const fks_tensor* t, int32_t nt, int32_t k, size_t* bytes
   return guarded([&] {
     validate(t, nt);
     if (!bytes || k < 0) throw Error(-FKS_EINVAL, "bad arguments");
-    const Layout L = make_layout(t, nt);
+    *bytes = workspace_total(t, nt, k, 0);
+  });
+}
+
+int fks_delta_workspace_size(const fks_tensor* t, int32_t nt, int32_t k, size_t* bytes) {
+  return guarded([&] {
+    validate(t, nt);
+    if (!bytes || k < 0) throw Error(-FKS_EINVAL, "bad arguments");
+    // any 8-byte aligned delta base gives the same layout; fks_delta_apply's tensor
+    // descriptors fit in the same workspace
+    *bytes = std::max(workspace_total(t, nt, k, 256), sizeof(DeltaApplyDesc) * (size_t)std::max(nt, 1) + 256);
+  });
+}
+
+int fks_delta_accumulate(const fks_tensor* t, int32_t nt, const uint64_t* seeds, const double* coefs, int32_t k,
+                         float* delta, void* workspace, size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    if (k > 0 && (!delta || ((uintptr_t)delta % 8) != 0)) throw Error(-FKS_EINVAL, "null or misaligned delta buffer");
+    run(t, nt, seeds, coefs, k, FKS_VALUE_SCALAR, kModeDelta, workspace, ws_bytes, stream, nullptr, 0, 1,
+        (uint64_t)(uintptr_t)delta);
+  });
+}
+
+int fks_delta_apply(const fks_tensor* t, int32_t nt, const float* delta, const double* decay, void* workspace,
+                    size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    validate(t, nt);
+    if (nt == 0) return;
+    if (!delta || !decay || !workspace) throw Error(-FKS_EINVAL, "null argument");
+    std::vector<DeltaApplyDesc> d;
+    int64_t cum = 0, maxn = 0;
+    for (int i = 0; i < nt; i++) {
+      if (t[i].numel > 0 && !(t[i].flags & FKS_FROZEN)) {
+        DeltaApplyDesc x{};
+        x.ptr = (uint64_t)(uintptr_t)t[i].data;
+        x.numel = t[i].numel;
+        x.delta_off = cum;
+        x.dtype = t[i].dtype;
+        x.decay = (float)decay[i];
+        d.push_back(x);
+        maxn = std::max(maxn, t[i].numel);
+      }
+      cum += t[i].numel;
+    }
+    if (d.empty()) return;
+    const size_t need = sizeof(DeltaApplyDesc) * d.size();
+    if (ws_bytes < need) throw Error(-FKS_EINVAL, "workspace too small");
+    thread_local std::vector<uint8_t> host;
+    host.assign(need, 0);
+    std::memcpy(host.data(), d.data(), need);
+    hipError_t e = hipMemcpyAsync(workspace, host.data(), need, hipMemcpyHostToDevice, (hipStream_t)stream);
+    if (e != hipSuccess) throw Error(-FKS_EHIP, std::string("hipMemcpyAsync: ") + hipGetErrorString(e));
+    const int rc = launch_delta_apply(static_cast<const DeltaApplyDesc*>(workspace), (int)d.size(), maxn, delta, stream);
+    if (rc) throw Error(-FKS_EHIP, std::string("fks_delta_apply_kernel launch: ") + hipGetErrorString((hipError_t)rc));
+  });
+}
+
+}  // extern "C"
+
+namespace fks {
+namespace {
+size_t workspace_total(const fks_tensor* t, int nt, int k, uint64_t delta_base) {
+  {
+    const Layout L = make_layout(t, nt, nullptr, delta_base);
     // upper bounds over every shard count: a shard never needs more chunks, segments,
     // runs or single elements than the whole stream
     WsSizes z;
@@ -570,9 +644,13 @@ int fks_workspace_size(const fks_tensor* t, int32_t nt, int32_t k, size_t* bytes
     z.nruns = (int)L.runs.size();
     z.ntiny = (int)L.tiny.size();
     z.k = std::max(k, 1);
-    *bytes = ws_layout(z).total;
-  });
+    return ws_layout(z).total;
+  }
 }
+}  // namespace
+}  // namespace fks
+
+extern "C" {
 
 int fks_directional_step(const fks_tensor* t, int32_t nt, const uint64_t* seeds, const double* values, int32_t k,
                          int32_t value_kind, void* workspace, size_t ws_bytes, void* stream) {

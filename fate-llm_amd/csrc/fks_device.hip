@@ -254,6 +254,7 @@ template <int DT>
 __device__ __forceinline__ float apply_one(float p, float z, float g, float lr, float wd, bool has_wd, int mode,
                                            float ps) {
   using TR = Traits<DT>;
+  if (mode == kModeDelta) return __fmaf_rn(g, z, p);   // seed-sharded variant: delta += c_k * z (f32)
   if (mode == kModePerturb || mode == kModePerturbUpdate) {
     p = TR::rnd(p + TR::rnd(ps * z));                  // param.data + scaling_factor * eps * z
     if (mode == kModePerturb) return p;
@@ -563,6 +564,10 @@ __device__ __forceinline__ f32x2_t rnd2(f32x2_t x) {
 template <int DT, int MODE>
 __device__ __forceinline__ f32x2_t apply_pair(f32x2_t p, f32x2_t z, float g, float lr, float wd, bool has_wd,
                                               float ps) {
+  if (MODE == kModeDelta) {  // delta += c_k * z: one v_pk_fma_f32 per element pair and seed
+    const f32x2_t gg = {g, g};
+    return __builtin_elementwise_fma(gg, z, p);
+  }
   if (MODE == kModePerturb || MODE == kModePerturbUpdate) {
     p = rnd2<DT>(p + rnd2<DT>(ps * z));
     if (MODE == kModePerturb) return p;
@@ -744,8 +749,11 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
   // that belong to each other (one DPP op) -- one dword (bf16) / dwordx2 (f32) access
   // per lane instead of two scattered ones.
   const bool odd = (tid & 1) != 0;
-  constexpr int kEs = DT == FKS_F32 ? 4 : 2;
-  typedef typename Traits<DT>::Pair Pair;
+  // storage: the parameters, or (kModeDelta) the f32 delta buffer the z of dtype DT is
+  // accumulated into
+  using ST = Traits<MODE == kModeDelta ? FKS_F32 : DT>;
+  constexpr int kEs = (DT == FKS_F32 || MODE == kModeDelta) ? 4 : 2;
+  typedef typename ST::Pair Pair;
   struct Slot { uint64_t addr; float lr, wd, ps; uint32_t wdf, on; Pair raw; };
   auto fetch = [&](int64_t b) -> Slot {
     Slot sl;
@@ -760,7 +768,7 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
     // compiler wait for it)
     sl.addr = on ? seg_ptr + (uint64_t)(s1 - seg_start + (odd ? 7 : 0)) * kEs : (uint64_t)(uintptr_t)a.sink;
     sl.raw = 0;
-    if (MODE != kModeWriteZ) sl.raw = Traits<DT>::load_pair(sl.addr);
+    if (MODE != kModeWriteZ) sl.raw = ST::load_pair(sl.addr);
     return sl;
   };
   // One block: twist, prefetch block b+1 (returned), Box-Muller + update chain, store.
@@ -771,22 +779,22 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
     const Slot nxt = fetch(b + 1 < b1 ? b + 1 : b);  // (the last block re-reads itself, unused)
     if (FKS_DIAG != 1) {  // every lane: off lanes compute garbage into the sink
       // even lane holds (p1, partner's p1), odd lane (partner's p2, p2)
-      const uint32_t keep = odd ? Traits<DT>::hi(sl.raw) : Traits<DT>::lo(sl.raw);
-      const uint32_t got = swap_adjacent(odd ? Traits<DT>::lo(sl.raw) : Traits<DT>::hi(sl.raw));
-      float p1 = Traits<DT>::cvt(odd ? got : keep), p2 = Traits<DT>::cvt(odd ? keep : got);
+      const uint32_t keep = odd ? ST::hi(sl.raw) : ST::lo(sl.raw);
+      const uint32_t got = swap_adjacent(odd ? ST::lo(sl.raw) : ST::hi(sl.raw));
+      float p1 = ST::cvt(odd ? got : keep), p2 = ST::cvt(odd ? keep : got);
       if constexpr (FULL) {
         pair_all<DT, MODE, kMaxSeedsPerPass>(lds, st_off, gk, sl.lr, sl.wd, sl.wdf != 0, sl.ps, p1, p2);
       } else {
         for (int k = 0; k < nseeds; k++)
           pair_one<DT, MODE>(lds, st_off, k, gk[k], sl.lr, sl.wd, sl.wdf != 0, sl.ps, p1, p2);
       }
-      const uint32_t b1v = Traits<DT>::bits(p1), b2v = Traits<DT>::bits(p2);
+      const uint32_t b1v = ST::bits(p1), b2v = ST::bits(p2);
       const uint32_t back = swap_adjacent(odd ? b1v : b2v);  // even gets partner's p1, odd partner's p2
-      const Pair out = odd ? Traits<DT>::pack(back, b2v) : Traits<DT>::pack(b1v, back);
+      const Pair out = odd ? ST::pack(back, b2v) : ST::pack(b1v, back);
 #if FKS_DIAG == 6
       if (p1 == 1234.5f && p2 == -99.25f)
 #endif
-      Traits<DT>::store_pair(sl.addr, out);
+      ST::store_pair(sl.addr, out);
     }
     return nxt;
   };
@@ -876,7 +884,7 @@ __device__ __forceinline__ void irr_z_pair(const uint8_t* lds, uint32_t r1, uint
 template <int DT, int MODE>
 __device__ __forceinline__ void irr_run_lane(const uint8_t* lds, const uint32_t* win, const IrrArgs& a, const DevRun& R,
                                              int64_t e1, int w1) {
-  using TR = Traits<DT>;
+  using TR = Traits<MODE == kModeDelta ? FKS_F32 : DT>;  // storage (kModeDelta: the f32 delta)
   const bool on1 = e1 < R.limit, on2 = e1 + 8 < R.limit;
   float p1 = 0.0f, p2 = 0.0f;
   if (MODE != kModeWriteZ) {
@@ -902,7 +910,7 @@ __device__ __forceinline__ double u53(uint32_t hi, uint32_t lo) {  // uniform_re
 
 template <int DT, int MODE>
 __device__ __forceinline__ void irr_tiny_lane(const uint32_t* win, const IrrArgs& a, const DevTiny& T, int w) {
-  using TR = Traits<DT>;
+  using TR = Traits<MODE == kModeDelta ? FKS_F32 : DT>;  // storage (kModeDelta: the f32 delta)
   float p = MODE != kModeWriteZ ? TR::load(T.ptr, 0) : 0.0f;
   const bool has_wd = (T.flags & FKS_HAS_WD) != 0;
   const bool sin_half = (T.flags & kTinySin) != 0;
@@ -914,7 +922,7 @@ __device__ __forceinline__ void irr_tiny_lane(const uint32_t* win, const IrrArgs
     const double theta = 2.0 * 3.14159265358979323846 * u1;
     const double v = (sin_half ? r * sin(theta) : r * cos(theta)) * 1.0 + 0.0;
     const float zf = (float)v;  // static_cast<scalar_t>(double): via float for bf16 / f16
-    const float z = DT == FKS_F32 ? zf : TR::rnd(zf);
+    const float z = DT == FKS_F32 ? zf : Traits<DT>::rnd(zf);
     p = apply_one<DT>(p, z, g[k], T.lr, T.wd, has_wd, MODE, T.ps);
   }
   TR::store(T.ptr, 0, p);
@@ -1010,9 +1018,39 @@ __global__ __launch_bounds__(kApplyThreads) void fks_irregular_kernel(IrrArgs a)
   }
 }
 
+// ------------------------------------------------------------------ delta apply
+// Seed-sharded variant, last step: p_K = a^K p_0 - delta (delta = sum_k lr g_k
+// a^(K-1-k) z_k, a = 1 - lr wd, all-reduced over the ranks), one fma in f32 and one
+// rounding to the parameter dtype.  grid (x, tensors): each row walks one tensor.
+template <int DT>
+__device__ __forceinline__ void delta_apply_one(const DeltaApplyDesc& D, const float* delta, int64_t e) {
+  using TR = Traits<DT>;
+  const float p = TR::load(D.ptr, e);
+  TR::store(D.ptr, e, TR::rnd(__fmaf_rn(D.decay, p, -delta[D.delta_off + e])));
+}
+
+__global__ __launch_bounds__(256) void fks_delta_apply_kernel(const DeltaApplyDesc* d, const float* delta) {
+  const DeltaApplyDesc D = d[blockIdx.y];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < D.numel; e += stride) {
+    switch (D.dtype) {
+      case FKS_F32: delta_apply_one<FKS_F32>(D, delta, e); break;
+      case FKS_BF16: delta_apply_one<FKS_BF16>(D, delta, e); break;
+      default: delta_apply_one<FKS_F16>(D, delta, e); break;
+    }
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
+int launch_delta_apply(const DeltaApplyDesc* d, int n, int64_t max_numel, const float* delta, void* stream) {
+  const int64_t blocks = std::min<int64_t>(std::max<int64_t>(1, (max_numel + 255) / 256), 2048);
+  hipLaunchKernelGGL(fks_delta_apply_kernel, dim3((unsigned)blocks, (unsigned)n), dim3(256), 0, (hipStream_t)stream,
+                     d, delta);
+  return (int)hipGetLastError();
+}
+
 static size_t apply_lds_bytes() { return (size_t)kLdsTabBytes + (size_t)kLdsStBytes; }
 
 int device_cu_count() {
@@ -1092,12 +1130,14 @@ int launch_apply(int dtype, const ApplyArgs& a, void* stream) {
     case FKS_F32 * 8 + kModePerturb: return launch_apply_t<FKS_F32, kModePerturb>(a, stream);
     case FKS_F32 * 8 + kModePerturbUpdate: return launch_apply_t<FKS_F32, kModePerturbUpdate>(a, stream);
     case FKS_F32 * 8 + kModeWriteZ: return launch_apply_t<FKS_F32, kModeWriteZ>(a, stream);
+    case FKS_F32 * 8 + kModeDelta: return launch_apply_t<FKS_F32, kModeDelta>(a, stream);
     case FKS_BF16 * 8 + kModeUpdate: return launch_apply_t<FKS_BF16, kModeUpdate>(a, stream);
     case FKS_BF16 * 8 + kModeUpdateWd: return launch_apply_t<FKS_BF16, kModeUpdateWd>(a, stream);
     case FKS_BF16 * 8 + kModeUpdateNoWd: return launch_apply_t<FKS_BF16, kModeUpdateNoWd>(a, stream);
     case FKS_BF16 * 8 + kModePerturb: return launch_apply_t<FKS_BF16, kModePerturb>(a, stream);
     case FKS_BF16 * 8 + kModePerturbUpdate: return launch_apply_t<FKS_BF16, kModePerturbUpdate>(a, stream);
     case FKS_BF16 * 8 + kModeWriteZ: return launch_apply_t<FKS_BF16, kModeWriteZ>(a, stream);
+    case FKS_BF16 * 8 + kModeDelta: return launch_apply_t<FKS_BF16, kModeDelta>(a, stream);
     default: return -FKS_ENOTSUP;
   }
 }
@@ -1126,6 +1166,7 @@ int launch_irregular(const IrrArgs& a, void* stream) {
     case kModePerturb: return launch_irregular_m<kModePerturb>(a, stream);
     case kModePerturbUpdate: return launch_irregular_m<kModePerturbUpdate>(a, stream);
     case kModeWriteZ: return launch_irregular_m<kModeWriteZ>(a, stream);
+    case kModeDelta: return launch_irregular_m<kModeDelta>(a, stream);
     default: return -FKS_ENOTSUP;
   }
 }

@@ -97,8 +97,11 @@ constexpr int kJumpXLen = 19937 + 624;  // x[0..20560]: y[i + w] = x[i + w + 1],
 // all have / all lack the weight-decay term (fast kernel only; chosen by the host)
 // kModePerturbUpdate: p + ps*z, then the update with the same z (the restore
 // perturbation of zeroth_order_step fused with its directional step)
+// kModeDelta: the seed-sharded variant; z is accumulated into an f32 delta buffer,
+// delta += c_k * z (one fma), instead of updating the parameters
 enum ApplyMode : int {
-  kModeUpdate = 0, kModePerturb = 1, kModeWriteZ = 2, kModeUpdateWd = 3, kModeUpdateNoWd = 4, kModePerturbUpdate = 5
+  kModeUpdate = 0, kModePerturb = 1, kModeWriteZ = 2, kModeUpdateWd = 3, kModeUpdateNoWd = 4, kModePerturbUpdate = 5,
+  kModeDelta = 6
 };
 
 struct ApplyArgs {
@@ -137,10 +140,21 @@ struct JumpArgs {
   int32_t chunks_per_wg;
 };
 
+// fks_delta_apply: p = dtype(f32(decay) * p - delta[delta_off + e]) over one tensor
+struct DeltaApplyDesc {
+  uint64_t ptr;       // the tensor's parameters
+  int64_t numel;
+  int64_t delta_off;  // its first element in the delta buffer
+  int32_t dtype;
+  float decay;        // (1 - lr*wd)^K, or 1 without the weight-decay term
+};
+static_assert(sizeof(DeltaApplyDesc) == 32, "DeltaApplyDesc layout");
+
 // launchers (fks_device.hip); return hipError_t as int
 int launch_jump(const JumpArgs& a, int nseeds, void* stream);
 int launch_apply(int dtype, const ApplyArgs& a, void* stream);
 int launch_irregular(const IrrArgs& a, void* stream);
+int launch_delta_apply(const DeltaApplyDesc* d, int n, int64_t max_numel, const float* delta, void* stream);
 int device_cu_count();
 
 }  // namespace fks

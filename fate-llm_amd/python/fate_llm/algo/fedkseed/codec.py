@@ -84,10 +84,11 @@ class _Batch:
         self.arr = arr
         self.n = len(self.specs)
 
-    def workspace(self, k: int):
+    def workspace(self, k: int, delta: bool = False):
         L = N.load()
         nbytes = ctypes.c_size_t(0)
-        N.check(L.fks_workspace_size(ctypes.addressof(self.arr), self.n, int(k), ctypes.byref(nbytes)))
+        size_fn = L.fks_delta_workspace_size if delta else L.fks_workspace_size
+        N.check(size_fn(ctypes.addressof(self.arr), self.n, int(k), ctypes.byref(nbytes)))
         ws = torch.empty(max(int(nbytes.value), 1), dtype=torch.uint8, device=self.device)
         return ws, int(nbytes.value)
 
@@ -193,6 +194,57 @@ def normal_(tensors: Sequence[torch.Tensor], seed: int, frozen: Optional[Sequenc
         ws, nbytes = b.workspace(1)
         N.check(L.fks_normal(ctypes.addressof(b.arr), b.n, _seed_u64(seed), ws.data_ptr(), nbytes,
                              _stream_handle(b.device)))
+        b.finish()
+
+
+def _check_delta(b: _Batch, delta: torch.Tensor) -> None:
+    total = sum(sp.tensor.numel() for sp in b.specs)
+    if delta.dtype != torch.float32 or not delta.is_contiguous() or delta.numel() != total:
+        raise ValueError(f"delta must be a contiguous float32 tensor of {total} elements (the tensors' concatenation)")
+    if delta.device != b.device:
+        raise ValueError("delta must live on the parameters' device")
+
+
+def delta_accumulate(specs: Sequence[ParamSpec], seeds: Sequence[int], coefs: Sequence[float],
+                     delta: torch.Tensor) -> None:
+    """Seed-sharded variant (include/fks.h): delta += f32(coef_s) * z_s for every seed in
+    order, z_s the reference's stream for the spec list (frozen specs draw, are not
+    accumulated); delta is the f32 concatenation of the specs' elements."""
+    if len(seeds) != len(coefs):
+        raise ValueError("seeds and coefs differ in length")
+    specs = list(specs)
+    if not specs or not len(seeds):
+        return
+    b = _Batch(specs)
+    if b.device is None:
+        return
+    _check_delta(b, delta)
+    L = N.load()
+    s = np.ascontiguousarray([_seed_u64(x) for x in seeds], dtype=np.uint64)
+    c = np.ascontiguousarray([float(x) for x in coefs], dtype=np.float64)
+    with torch.cuda.device(b.device):
+        ws, nbytes = b.workspace(len(s), delta=True)
+        N.check(L.fks_delta_accumulate(ctypes.addressof(b.arr), b.n, s.ctypes.data, c.ctypes.data, len(s),
+                                       delta.data_ptr(), ws.data_ptr(), nbytes, _stream_handle(b.device)))
+
+
+def delta_apply(specs: Sequence[ParamSpec], delta: torch.Tensor, decays: Sequence[float]) -> None:
+    """p = dtype(f32(decay_i) * p - delta) per non-frozen spec (one fma, one rounding)."""
+    specs = list(specs)
+    if not specs:
+        return
+    if len(decays) != len(specs):
+        raise ValueError("one decay per spec")
+    b = _Batch(specs)
+    if b.device is None:
+        return
+    _check_delta(b, delta)
+    L = N.load()
+    d = np.ascontiguousarray([float(x) for x in decays], dtype=np.float64)
+    with torch.cuda.device(b.device):
+        ws, nbytes = b.workspace(1, delta=True)
+        N.check(L.fks_delta_apply(ctypes.addressof(b.arr), b.n, delta.data_ptr(), d.ctypes.data, ws.data_ptr(),
+                                  nbytes, _stream_handle(b.device)))
         b.finish()
 
 

@@ -73,6 +73,69 @@ def reconstruct_(param_groups: List[dict], seeds: Sequence[int], values: Sequenc
     return len(keep)
 
 
+def seed_shard_coefficients(values: Sequence[float], lr: float, weight_decay, rank: int = 0, world: int = 1):
+    """Seed-sharded variant (BASELINE config C3): the K sequential steps
+    p <- p - lr*(g_k*z_k + wd*p) of the reconstruct sum to
+    p_K = a^K p_0 - sum_k lr g_k a^(K-1-k) z_k with a = 1 - lr*wd (a = 1 without the
+    decay term).  Returns (first, last) -- the seed index range [first, last) rank
+    ``rank`` of ``world`` accumulates, a contiguous 1/world of the K seeds -- the
+    coefficients lr g_k a^(K-1-k) of that range (float64), and a^K.
+    lr and wd enter as the fp32 values the reference's opmath sees."""
+    import math
+
+    import numpy as np
+
+    k = len(values)
+    first, last = k * rank // world, k * (rank + 1) // world
+    lr32 = float(np.float32(lr))
+    if weight_decay is None:
+        log_a = 0.0
+    else:
+        log_a = math.log1p(-lr32 * float(np.float32(weight_decay)))
+    coefs = [lr32 * float(values[i]) * math.exp((k - 1 - i) * log_a) for i in range(first, last)]
+    return first, last, coefs, math.exp(k * log_a)
+
+
+def reconstruct_seed_sharded_(param_groups: List[dict], seeds: Sequence[int], values: Sequence[float], lr: float,
+                              weight_decay: float, process_group=None, delta: torch.Tensor = None) -> int:
+    """The reconstruct of ClientTrainer.train_once as the north star's seed-sharded
+    variant: every rank of ``process_group`` (torch.distributed, RCCL on MI355X) takes a
+    contiguous 1/world of the non-zero seeds, accumulates its part of the f32 delta on
+    its GPU, one all-reduce sums the parts, and every rank applies p = a^K p_0 - delta.
+
+    NOT bit-equal to ``reconstruct_`` / the reference (which rounds every op of every
+    seed to the parameter dtype): see DESIGN.md §7 for the measured deviation.  All
+    tensors must share one (lr, wd) -- train_once passes them explicitly, so the sticky
+    rule makes them uniform.  ``delta``: optional preallocated f32 buffer (the
+    parameters' concatenation), zeroed here.  Returns the number of seeds applied."""
+    import torch.distributed as dist
+
+    keep = [(int(s), float(g)) for s, g in zip(seeds, values) if float(g) != 0.0]
+    if not keep:
+        return 0
+    specs = codec.resolve_groups(param_groups, lr=lr, weight_decay=weight_decay)
+    classes = {(sp.lr, sp.weight_decay) for sp in specs}
+    if len(classes) != 1:
+        raise ValueError("seed-sharded reconstruct needs one (lr, weight_decay) for every tensor")
+    distributed = process_group is not None or (dist.is_available() and dist.is_initialized())
+    rank = dist.get_rank(process_group) if distributed else 0
+    world = dist.get_world_size(process_group) if distributed else 1
+    sp0 = specs[0]
+    first, last, coefs, decay = seed_shard_coefficients([g for _, g in keep], sp0.lr, sp0.weight_decay, rank, world)
+    total = sum(sp.tensor.numel() for sp in specs)
+    dev = sp0.tensor.device
+    if delta is None:
+        delta = torch.zeros(total, dtype=torch.float32, device=dev)
+    else:
+        delta.zero_()
+    codec.delta_accumulate(specs, [s for s, _ in keep[first:last]], coefs, delta)
+    if world > 1:
+        dist.all_reduce(delta, op=dist.ReduceOp.SUM, group=process_group)
+    codec.delta_apply(specs, delta, [decay] * len(specs))
+    torch.manual_seed(keep[-1][0])
+    return len(keep)
+
+
 def build_seed_candidates(k, low=0, high=2**32):
     """K seed candidates drawn from the global torch generator."""
     return torch.randint(low, high, size=(k,), dtype=torch.long)

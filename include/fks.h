@@ -131,6 +131,29 @@ int fks_perturb(const fks_tensor* t, int32_t nt, uint64_t seed, const double* sc
 int fks_perturb_step(const fks_tensor* t, int32_t nt, uint64_t seed, const double* scales, double value,
                      int32_t value_kind, int32_t update, void* workspace, size_t ws_bytes, void* stream);
 
+/* ---- seed-sharded variant (BASELINE config C3) ----
+ * The reconstruct loop of ClientTrainer.train_once (fedkseed.py:136-141) applies K
+ * seeds in order, p <- p - lr*(g_k*z_k + wd*p), i.e. with a = 1 - lr*wd
+ *     p_K = a^K p_0 - sum_k lr g_k a^(K-1-k) z_k.
+ * Ranks can split the seeds, accumulate their part of the sum in f32 and all-reduce it
+ * (one RCCL call), then every rank applies p_K.  This is NOT the reference's rounding
+ * (the reference rounds every op of every seed to the parameter dtype); it is the
+ * variant the north star names, reported with its measured deviation.
+ *
+ * fks_delta_accumulate: for s = 0..k-1 in order, for every non-frozen tensor i and
+ * element e: delta[cum_i + e] = fmaf(f32(coefs[s]), z_s(i, e), delta[cum_i + e]),
+ * cum_i = sum of numel over tensors before i (the delta buffer is the tensors'
+ * concatenation, f32, 8-byte aligned, device memory); z_s is the reference's stream
+ * for seeds[s] and the tensor's dtype.  lr/wd/flags of the tensors are ignored (the
+ * caller folds them into coefs).  Workspace: fks_delta_workspace_size.
+ * fks_delta_apply: for every non-frozen tensor i: p = dtype(fmaf(f32(decay[i]), p,
+ * -delta[cum_i + e])).                                                               */
+int fks_delta_workspace_size(const fks_tensor* t, int32_t nt, int32_t k, size_t* bytes);
+int fks_delta_accumulate(const fks_tensor* t, int32_t nt, const uint64_t* seeds, const double* coefs, int32_t k,
+                         float* delta, void* workspace, size_t ws_bytes, void* stream);
+int fks_delta_apply(const fks_tensor* t, int32_t nt, const float* delta, const double* decay, void* workspace,
+                    size_t ws_bytes, void* stream);
+
 /* torch.manual_seed(seed); for every tensor in order: p = torch.normal(0, 1, size, dtype). */
 int fks_normal(const fks_tensor* t, int32_t nt, uint64_t seed, void* workspace, size_t ws_bytes, void* stream);
 

@@ -552,5 +552,66 @@ int fko_perturb_params(const fko_tensor *t, int32_t nt, uint64_t seed, double sc
     return 0;
 }
 
+/* ------------------------------------------------------------------------- */
+/* Seed-sharded variant (include/fks.h fks_delta_accumulate / fks_delta_apply): */
+/* NOT a reference routine -- the restated sum p_K = a^K p_0 - sum_k c_k z_k of */
+/* the reference's K sequential steps (zo_utils.py:49 with a = 1 - lr*wd), with */
+/* the device's exact f32 operation order, so its kernels can be checked bit    */
+/* for bit.  z is the reference's stream (fedkseed.py:138 -> zo_utils.py:47).   */
+/* ------------------------------------------------------------------------- */
+static float z_as_float(const void *z, int64_t e, int dtype) {
+    if (dtype == FKO_F32) return ((const float *)z)[e];
+    if (dtype == FKO_BF16) return f_from_bf16(((const uint16_t *)z)[e]);
+    return f_from_h(((const uint16_t *)z)[e]);
+}
+
+/* delta[cum_i + e] = fmaf(f32(coefs[s]), z_s(i, e), delta[cum_i + e]) for s in order;
+ * frozen[i] != 0: the tensor draws its z but its delta is not written */
+int fko_delta_accumulate(const fko_tensor *t, int32_t nt, const int32_t *frozen, const uint64_t *seeds,
+                         const double *coefs, int32_t k, float *delta, int32_t capability) {
+    int64_t maxn = 16;
+    for (int i = 0; i < nt; i++) if (t[i].numel > maxn) maxn = t[i].numel;
+    void *z = malloc((size_t)maxn * 8);
+    if (!z) return -12;
+    fko_gen gen;
+    for (int s = 0; s < k; s++) {
+        const float c = (float)coefs[s];
+        fko_seed(&gen, seeds[s]);
+        int64_t cum = 0;
+        for (int i = 0; i < nt; i++) {
+            fko_normal(&gen, z, t[i].numel, t[i].dtype, capability);
+            if (!(frozen && frozen[i]))
+                for (int64_t e = 0; e < t[i].numel; e++)
+                    delta[cum + e] = fmaf(c, z_as_float(z, e, t[i].dtype), delta[cum + e]);
+            cum += t[i].numel;
+        }
+    }
+    free(z);
+    return 0;
+}
+
+/* p = dtype(fmaf(f32(decay[i]), p, -delta[cum_i + e])) */
+void fko_delta_apply(const fko_tensor *t, int32_t nt, const int32_t *frozen, const float *delta, const double *decay) {
+    int64_t cum = 0;
+    for (int i = 0; i < nt; i++) {
+        if (!(frozen && frozen[i])) {
+            const float d = (float)decay[i];
+            for (int64_t e = 0; e < t[i].numel; e++) {
+                if (t[i].dtype == FKO_F32) {
+                    float *p = (float *)t[i].data;
+                    p[e] = fmaf(d, p[e], -delta[cum + e]);
+                } else if (t[i].dtype == FKO_BF16) {
+                    uint16_t *p = (uint16_t *)t[i].data;
+                    p[e] = bf16_from_f(fmaf(d, f_from_bf16(p[e]), -delta[cum + e]));
+                } else {
+                    uint16_t *p = (uint16_t *)t[i].data;
+                    p[e] = h_from_f(fmaf(d, f_from_h(p[e]), -delta[cum + e]));
+                }
+            }
+        }
+        cum += t[i].numel;
+    }
+}
+
 int fko_sizeof_gen(void) { return (int)sizeof(fko_gen); }
 int fko_sizeof_tensor(void) { return (int)sizeof(fko_tensor); }

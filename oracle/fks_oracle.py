@@ -58,6 +58,11 @@ def lib():
         L.fko_reconstruct.restype = ctypes.c_int
         L.fko_perturb_params.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64, ctypes.c_double,
                                          ctypes.c_int32]
+        L.fko_delta_accumulate.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
+        L.fko_delta_accumulate.restype = ctypes.c_int
+        L.fko_delta_apply.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p]
         L.fko_perturb_params.restype = ctypes.c_int
         L.fko_set_contract.argtypes = [ctypes.c_int]
         L.fko_sizeof_gen.restype = ctypes.c_int
@@ -160,3 +165,27 @@ def perturb_params(arrays, dtypes, seed: int, scale: float, capability: int = CA
 def set_contract(bits: int) -> None:
     """Select an FMA-contraction variant (-1 = pinned default); for the pinning search only."""
     lib().fko_set_contract(int(bits))
+
+
+def delta_accumulate(arrays, dtypes, seeds, coefs, delta: np.ndarray, frozen=None,
+                     capability: int = CAP_AVX2) -> None:
+    """Seed-sharded variant (not a reference routine): delta (f32, the arrays'
+    concatenation) += f32(coef_s) * z_s, one fmaf per element and seed, seeds in order."""
+    assert delta.dtype == np.float32 and delta.flags.c_contiguous
+    assert delta.size == sum(a.size for a in arrays)
+    T = _tensor_array(arrays, dtypes, [0.0] * len(arrays), [None] * len(arrays))
+    fz = np.ascontiguousarray(np.asarray(frozen if frozen is not None else [0] * len(arrays), dtype=np.int32))
+    s = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint64))
+    c = np.ascontiguousarray(np.asarray(coefs, dtype=np.float64))
+    rc = lib().fko_delta_accumulate(ctypes.addressof(T), len(arrays), fz.ctypes.data, s.ctypes.data, c.ctypes.data,
+                                    len(s), delta.ctypes.data, capability)
+    if rc != 0:
+        raise RuntimeError(f"fko_delta_accumulate failed: {rc}")
+
+
+def delta_apply(arrays, dtypes, delta: np.ndarray, decays, frozen=None) -> None:
+    """p = dtype(fmaf(f32(decay_i), p, -delta)) per tensor, in place."""
+    T = _tensor_array(arrays, dtypes, [0.0] * len(arrays), [None] * len(arrays))
+    fz = np.ascontiguousarray(np.asarray(frozen if frozen is not None else [0] * len(arrays), dtype=np.int32))
+    d = np.ascontiguousarray(np.asarray(decays, dtype=np.float64))
+    lib().fko_delta_apply(ctypes.addressof(T), len(arrays), fz.ctypes.data, delta.ctypes.data, d.ctypes.data)

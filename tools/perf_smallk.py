@@ -1,0 +1,65 @@
+"""Small-K cost on the 7B bf16 layout (the ZO local step's perturb / update calls):
+wall time per call (synchronised), device time of the apply and jump kernels, and the
+host-side share.  python tools/perf_smallk.py [--params N] [--reps R]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fate-llm_amd", "python"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--params", type=int, default=0)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--ks", default="1,2,4,8,19")
+    args = ap.parse_args()
+    from fate_llm.algo.fedkseed import codec
+
+    dev = torch.device("cuda", 0)
+    shapes = [(args.params,)] if args.params else bench.llama7b_shapes()
+    total = sum(bench.numel(s) for s in shapes)
+    flat = torch.empty(total, dtype=torch.bfloat16, device=dev).normal_(0.0, 0.02)
+    views, off = [], 0
+    for s in shapes:
+        views.append(flat[off:off + bench.numel(s)].view(s))
+        off += bench.numel(s)
+    specs = [codec.ParamSpec(v, lr=1e-5, weight_decay=0.01) for v in views]
+    seeds, scalars = bench.synthetic_seeds(64)
+    scalars = [g if g != 0.0 else 1.0 for g in scalars]
+
+    def measure(name, fn):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with codec.profile() as prof:
+            for _ in range(args.reps):
+                fn()
+            torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / args.reps * 1e3
+        t1 = time.perf_counter()
+        for _ in range(args.reps):
+            fn()
+        host = (time.perf_counter() - t1) / args.reps * 1e3  # enqueue only (async)
+        torch.cuda.synchronize()
+        rec = {"call": name, "wall_ms": round(wall, 3), "apply_ms": round(prof.apply_ms / args.reps, 3),
+               "jump_ms": round(prof.jump_ms / args.reps, 3), "enqueue_ms": round(host, 3),
+               "GBps": round(total * 2 / wall * 1e-6, 1)}
+        print(json.dumps(rec), flush=True)
+
+    measure("perturb", lambda: codec.perturb(views, seeds[0], 5e-4))
+    measure("perturb_step", lambda: codec.perturb_step(specs, seeds[0], [5e-4] * len(specs), 1.5))
+    for k in [int(x) for x in args.ks.split(",")]:
+        measure(f"directional_step K={k}", lambda: codec.directional_step(specs, seeds[:k], scalars[:k]))
+
+
+if __name__ == "__main__":
+    main()
