@@ -29,6 +29,12 @@
 #ifndef FKS_UNROLL2
 #define FKS_UNROLL2 0  // apply block loop unrolled by two (slots swap roles)
 #endif
+#ifndef FKS_T64
+#define FKS_T64 1  // bf16 pair tempering on the 64-bit word pair (v_lshrrev_b64 / v_lshlrev_b64)
+#endif
+#ifndef FKS_RPAIR
+#define FKS_RPAIR 0  // radius table as (R,R) pairs read with ds_read_b64 (else R[256] f32, ds_read_b32)
+#endif
 
 namespace fks {
 namespace {
@@ -516,22 +522,77 @@ __device__ __forceinline__ void twist_all(const TwistPlan& P, int nseeds) {
 __constant__ float c_tab_bf16[3 * 256];  // R | C | S, set once from fks::tables()
 
 // LDS: [R[256] f32 | (C,S)[256] f32x2 | windows (kMaxSeedsPerPass + 1) x 624 u32]
-constexpr int kLdsTabBytes = 256 * 4 + 256 * 8;
+// (FKS_RPAIR: R stored twice per 8-byte entry, same index scale as (C,S); measured 8 %
+// slower: the radius lookup moves twice the LDS bytes)
+constexpr int kLdsRBytes = FKS_RPAIR ? 256 * 8 : 256 * 4;
+constexpr int kLdsTabBytes = kLdsRBytes + 256 * 8;
+constexpr int kLdsCsOff = kLdsRBytes;
 constexpr int kLdsStBytes = (kMaxSeedsPerPass + 1) * kMtN * 4;
+
+// 64-bit shifts of a word pair held in one VGPR pair (full rate on gfx950, measured
+// tools/ubench): the bits one word shifts into the other are masked off afterwards
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+template <int S>
+__device__ __forceinline__ u32x2_t shr64(u32x2_t x) {
+  u32x2_t r;
+  asm("v_lshrrev_b64 %0, %2, %1" : "=v"(r) : "v"(x), "i"(S));
+  return r;
+}
+template <int S>
+__device__ __forceinline__ u32x2_t shl64(u32x2_t x) {
+  u32x2_t r;
+  asm("v_lshlrev_b64 %0, %2, %1" : "=v"(r) : "v"(x), "i"(S));
+  return r;
+}
+
+// Both table byte offsets (x8) of a Box-Muller word pair y = (word j, word j+8):
+// MT19937RNGEngine.h:141-145 tempering of both words, then ((y ^ (y >> 18)) & 0xFF) << 3,
+// 13 VALU ops for the two words instead of 18.  y >> 11 pulls 11 bits of the high word
+// into the top of the low one (mask 0x001FFFFF); y << 7 and y << 15 push the low word's
+// top bits into the high word's bits 0..6 / 0..14, which the tempering masks already
+// clear; the final shifts' spill lies outside 0x7F8.
+__device__ __forceinline__ u32x2_t temper_pair_u8x8(u32x2_t y) {
+  u32x2_t t = shr64<11>(y);
+  y.x = __builtin_amdgcn_bitop3_b32(y.x, t.x, 0x001FFFFFu, kXorAnd);
+  y.y ^= t.y;
+  t = shl64<7>(y);
+  y.x = __builtin_amdgcn_bitop3_b32(y.x, t.x, 0x9d2c5680u, kXorAnd);
+  y.y = __builtin_amdgcn_bitop3_b32(y.y, t.y, 0x9d2c5680u, kXorAnd);
+  t = shl64<15>(y);
+  y.x = __builtin_amdgcn_bitop3_b32(y.x, t.x, 0xefc60000u, kXorAnd);
+  y.y = __builtin_amdgcn_bitop3_b32(y.y, t.y, 0xefc60000u, kXorAnd);
+  const u32x2_t t1 = shl64<3>(y), t2 = shr64<15>(y);
+  u32x2_t o;
+  o.x = __builtin_amdgcn_bitop3_b32(t1.x, t2.x, 0x7F8u, kXorMask);
+  o.y = __builtin_amdgcn_bitop3_b32(t1.y, t2.y, 0x7F8u, kXorMask);
+  return o;
+}
 
 // bf16 Box-Muller pair before the final rounding: (R[a] * C[b], R[a] * S[b]) + 0 as ONE
 // v_pk_fma_f32 (R*C is exact in f32: 8-bit x 8-bit significands; the +0 addend turns
-// -0 into +0 like normal_fill_16's "+ mean").  R at LDS 0, (C,S) pairs at LDS 1024.
+// -0 into +0 like normal_fill_16's "+ mean").  (R,R) pairs at LDS 0, (C,S) pairs at 2048.
 __device__ __forceinline__ f32x2_t z_pair_bf16_raw(uint32_t r1, uint32_t r2) {
-  const uint32_t a4 = mt_temper_u8x4(r1), b8 = mt_temper_u8x8(r2);
-#if FKS_DIAG >= 3  // diagnostics: no table lookups (wrong values)
-  const float r = __uint_as_float(a4 | 0x3f800000u);
-  const f32x2_t cs = {__uint_as_float(b8 | 0x3f000000u), __uint_as_float(b8 | 0x3e000000u)};
+#if FKS_T64
+  u32x2_t w;
+  w.x = r1;
+  w.y = r2;
+  const u32x2_t ab = temper_pair_u8x8(w);
+  const uint32_t a8 = ab.x, b8 = ab.y;
 #else
-  const float r = lds_f32(a4);
-  const f32x2_t cs = lds_f32x2(1024 + b8);
+  const uint32_t a8 = mt_temper_u8x8(r1), b8 = mt_temper_u8x8(r2);
 #endif
-  const f32x2_t rr = {r, r}, zero = {0.0f, 0.0f};
+#if FKS_DIAG >= 3  // diagnostics: no table lookups (wrong values)
+  const f32x2_t rr = {__uint_as_float(a8 | 0x3f800000u), __uint_as_float(a8 | 0x3f800000u)};
+  const f32x2_t cs = {__uint_as_float(b8 | 0x3f000000u), __uint_as_float(b8 | 0x3e000000u)};
+#elif FKS_RPAIR
+  const f32x2_t rr = lds_f32x2(a8);
+  const f32x2_t cs = lds_f32x2(kLdsCsOff + b8);
+#else
+  const float r = lds_f32(a8 >> 1);
+  const f32x2_t rr = {r, r};
+  const f32x2_t cs = lds_f32x2(kLdsCsOff + b8);
+#endif
+  const f32x2_t zero = {0.0f, 0.0f};
   return __builtin_elementwise_fma(rr, cs, zero);
 }
 
@@ -629,22 +690,24 @@ __device__ __forceinline__ void pair_all(const uint8_t* lds, int st_off, const f
     uint32_t ia[NS], ib[NS];
 #pragma unroll
     for (int k = 0; k < NS; k++) {
-      ia[k] = mt_temper_u8x4(r1[k]);
+      ia[k] = mt_temper_u8x8(r1[k]);
       ib[k] = mt_temper_u8x8(r2[k]);
     }
     asm volatile("" ::: "memory");
-    float rr[NS];
+    f32x2_t rr[NS];
     f32x2_t cs[NS];
 #pragma unroll
     for (int k = 0; k < NS; k++) {
-      rr[k] = lds_f32(ia[k]);
-      cs[k] = lds_f32x2(1024 + ib[k]);
+      const float r = lds_f32(ia[k] >> 1);
+      rr[k].x = r;
+      rr[k].y = r;
+      cs[k] = lds_f32x2(kLdsCsOff + ib[k]);
     }
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int k = 0; k < NS; k++) {
-      const f32x2_t r2v = {rr[k], rr[k]}, zero = {0.0f, 0.0f};
-      z[k] = rnd2<DT>(__builtin_elementwise_fma(r2v, cs[k], zero));
+      const f32x2_t zero = {0.0f, 0.0f};
+      z[k] = rnd2<DT>(__builtin_elementwise_fma(rr[k], cs[k], zero));
     }
   } else {
 #pragma unroll
@@ -681,10 +744,10 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
   const int64_t b0 = a.chunk_block[c], b1 = a.chunk_block[c + 1];
 
   if constexpr (DT == FKS_BF16) {
-    float* tabR = reinterpret_cast<float*>(lds);
-    float2* tabCS = reinterpret_cast<float2*>(lds + 1024);
+    float2* tabCS = reinterpret_cast<float2*>(lds + kLdsCsOff);
     for (int i = tid; i < 256; i += kApplyThreads) {
-      tabR[i] = c_tab_bf16[i];
+      if (FKS_RPAIR) reinterpret_cast<float2*>(lds)[i] = make_float2(c_tab_bf16[i], c_tab_bf16[i]);
+      else reinterpret_cast<float*>(lds)[i] = c_tab_bf16[i];
       tabCS[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
     }
   }
@@ -940,10 +1003,10 @@ __global__ __launch_bounds__(kApplyThreads) void fks_irregular_kernel(IrrArgs a)
   const int nseeds = a.nseeds;
   const int64_t b0 = a.chunk_lo[c], b1 = a.chunk_hi[c];
   {
-    float* tabR = reinterpret_cast<float*>(lds);
-    float2* tabCS = reinterpret_cast<float2*>(lds + 1024);
+    float2* tabCS = reinterpret_cast<float2*>(lds + kLdsCsOff);
     for (int i = tid; i < 256; i += kApplyThreads) {
-      tabR[i] = c_tab_bf16[i];
+      if (FKS_RPAIR) reinterpret_cast<float2*>(lds)[i] = make_float2(c_tab_bf16[i], c_tab_bf16[i]);
+      else reinterpret_cast<float*>(lds)[i] = c_tab_bf16[i];
       tabCS[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
     }
   }

@@ -88,8 +88,8 @@ constexpr int kApplyThreads = 320;  // 312 Box-Muller pairs per 624-word block +
 #define FKS_APPLY_WG_PER_CU 3
 #endif
 constexpr int kApplyWgPerCu = FKS_APPLY_WG_PER_CU;  // resident apply workgroups per CU (LDS-limited)
-// MT windows resident in LDS per workgroup: (seeds + 1 spare) x 2496 B + 3 KB tables <= 160 KB / WGs
-constexpr int kMaxSeedsPerPass = (160 * 1024 / kApplyWgPerCu - 3072) / 2496 - 1;
+// MT windows resident in LDS per workgroup: (seeds + 1 spare) x 2496 B + 4 KB tables <= 160 KB / WGs
+constexpr int kMaxSeedsPerPass = (160 * 1024 / kApplyWgPerCu - 4096) / 2496 - 1;  // tables: <= 4 KB
 constexpr int kJumpThreads = 1024;  // 16 waves, one chunk's jump per wave at a time
 constexpr int kJumpXLen = 19937 + 624;  // x[0..20560]: y[i + w] = x[i + w + 1], i < 19937, w < 624
 

@@ -1,0 +1,51 @@
+"""A/B timing of apply-kernel builds: python tools/ab_apply.py [lib.so ...] (no argument:
+the in-tree libfks.so).  Each build runs in its own process (FKS_LIB_OVERRIDE) on the
+same workload -- N bf16 params (default 2^28), K seeds (default 95 = 5 full passes),
+wd on -- and prints the average apply/jump launch time per 19-seed pass."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r'''
+import os, sys, json, torch
+sys.path.insert(0, os.path.join(os.environ["ROOT"], "fate-llm_amd", "python"))
+from fate_llm.algo.fedkseed import codec
+n, k = int(os.environ["AB_N"]), int(os.environ["AB_K"])
+dt = torch.float32 if os.environ.get("AB_DT") == "f32" else torch.bfloat16
+buf = torch.empty(n, dtype=dt, device="cuda").normal_(0, 0.02)
+specs = [codec.ParamSpec(buf, lr=1e-5, weight_decay=0.01)]
+g = torch.Generator().manual_seed(1)
+seeds = torch.randint(0, 2**32, (k,), generator=g).tolist()
+vals = (torch.randn(k, generator=g, dtype=torch.float64) * 20).tolist()
+codec.directional_step(specs, seeds[:19], vals[:19]); torch.cuda.synchronize()
+best = None
+for _ in range(3):
+    with codec.profile() as p:
+        codec.directional_step(specs, seeds, vals); torch.cuda.synchronize()
+    r = p.apply_ms / max(p.n_apply, 1)
+    best = r if best is None else min(best, r)
+print(json.dumps({"lib": os.environ.get("FKS_LIB_OVERRIDE", "libfks.so"), "dtype": str(dt), "n": n, "k": k,
+                  "apply_ms_per_launch": round(best, 3),
+                  "ps_per_seed_param": round(best * 1e9 / (n * 19), 3)}), flush=True)
+'''
+
+
+def main():
+    libs = sys.argv[1:] or [""]
+    for lib in libs:
+        env = dict(os.environ, ROOT=ROOT, AB_N=os.environ.get("AB_N", str(1 << 28)),
+                   AB_K=os.environ.get("AB_K", "95"))
+        if lib:
+            env["FKS_LIB_OVERRIDE"] = os.path.abspath(lib)
+        else:
+            env.pop("FKS_LIB_OVERRIDE", None)
+        r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
+        out = [l for l in r.stdout.splitlines() if l.startswith("{")]
+        print(out[-1] if out else json.dumps({"lib": lib, "error": r.stderr[-500:]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
