@@ -73,8 +73,8 @@ def synthetic_seeds(k):
 
 def load_pmc_summary():
     """Per-launch HBM traffic and VALU lane-ops per seed-element of the apply kernel,
-    from the committed rocprofv3 --pmc pass (profiles/pmc_apply_r01.json)."""
-    p = os.path.join(ROOT, "profiles", "pmc_apply_r01.json")
+    from the committed rocprofv3 --pmc pass (profiles/pmc_apply_r01b.json)."""
+    p = os.path.join(ROOT, "profiles", "pmc_apply_r01b.json")
     try:
         with open(p) as f:
             return json.load(f)
@@ -200,7 +200,7 @@ def main():
         valu = {"bound": "valu", "achieved": round(ach, 3), "peak": VALU_PEAK_TLANEOPS, "unit": "Tlane-op/s",
                 "frac": round(ach / VALU_PEAK_TLANEOPS, 4), "lane_ops_per_unit": lane_ops,
                 "unit_def": "one seed*param update (z draw + update); lane-ops = rocprofv3 SQ_INSTS_VALU x 64 per "
-                            "seed*param (profiles/pmc_apply_r01.json); peak = non-packed VALU issue rate"}
+                            "seed*param (profiles/pmc_apply_r01b.json); peak = non-packed VALU issue rate"}
     traffic = None if seed_shard else pmc.get("hbm_bytes_per_param_per_launch")
     if seed_shard:
         valu = None  # the committed PMC summary is the sequential kernel's
