@@ -176,8 +176,11 @@ BlockRange shard_blocks(int64_t stream_len, int shard, int nshards) {
   return {(int64_t)((__int128)nb * shard / nshards), (int64_t)((__int128)nb * (shard + 1) / nshards)};
 }
 
-int plan_nchunks(int64_t nblocks) {
-  const int64_t target = (int64_t)kApplyWgPerCu * device_cu_count();  // one wave of apply workgroups
+// one wave of apply workgroups: kApplyWgPerCu per CU for the 19-seed passes, more for
+// calls of at most kSmallK seeds (little LDS per workgroup, so more independent streams
+// per CU hide the per-block latency chain)
+int plan_nchunks(int64_t nblocks, bool small = false) {
+  const int64_t target = (int64_t)(small ? kSmallWgPerCu : kApplyWgPerCu) * device_cu_count();
   return (int)std::max<int64_t>(1, std::min<int64_t>(nblocks, target));
 }
 
@@ -190,9 +193,9 @@ Plan plan_from_blocks(std::vector<int64_t> chunk_block) {
   return P;
 }
 
-Plan make_plan(BlockRange r) {
+Plan make_plan(BlockRange r, bool small) {
   const int64_t nblocks = std::max<int64_t>(1, r.hi - r.lo);
-  const int nchunks = plan_nchunks(nblocks);
+  const int nchunks = plan_nchunks(nblocks, small);
   std::vector<int64_t> cb((size_t)nchunks + 1);
   for (int c = 0; c <= nchunks; c++) cb[(size_t)c] = r.lo + (int64_t)((__int128)nblocks * c / nchunks);
   return plan_from_blocks(std::move(cb));
@@ -315,24 +318,25 @@ IrrChunks irregular_chunks(const Layout& L) {
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// Workspace: [header uploaded once per call | generator windows].  Both plans (fast
-// and irregular) share the window area: they run one after the other on the stream.
-struct WsSizes {
-  int reg_chunks = 0, irr_chunks = 0, nsegs = 0, nruns = 0, ntiny = 0, k = 0;
+// Static header of a call: everything that depends only on the tensor list, the
+// perturbation scales, the shard and the chunk policy -- the chunk table, the jump
+// polynomials and the segment / run / element descriptors.  It lives on the device in
+// the plan cache (PlanCache below) and is uploaded once per distinct tensor list; the
+// per-pass seeds and multipliers travel by value in the kernel arguments.
+struct HdrSizes {
+  int reg_chunks = 0, irr_chunks = 0, nsegs = 0, nruns = 0, ntiny = 0;
 };
 
-struct WsLayout {
-  size_t header = 0;  // bytes of the uploaded header
+struct HdrLayout {
   size_t off_polys = 0, off_cb = 0, off_ipolys = 0, off_ilo = 0, off_ihi = 0, off_segs = 0, off_runs = 0,
-         off_tiny = 0, off_seeds = 0, off_g = 0, off_sink = 0, off_states = 0;
+         off_tiny = 0;
   size_t total = 0;
 };
 
-WsLayout ws_layout(const WsSizes& z) {
-  WsLayout w;
+HdrLayout hdr_layout(const HdrSizes& z) {
+  HdrLayout w;
   size_t o = 0;
   auto put = [&](size_t& off, size_t bytes) { off = o; o = align_up(o + std::max<size_t>(bytes, 1), 256); };
-  const size_t k = (size_t)std::max(z.k, 1);
   put(w.off_polys, sizeof(uint64_t) * 312 * (size_t)z.reg_chunks);
   put(w.off_cb, sizeof(int64_t) * ((size_t)z.reg_chunks + 1));
   put(w.off_ipolys, sizeof(uint64_t) * 312 * (size_t)z.irr_chunks);
@@ -341,14 +345,14 @@ WsLayout ws_layout(const WsSizes& z) {
   put(w.off_segs, sizeof(DevSeg) * (size_t)z.nsegs);
   put(w.off_runs, sizeof(DevRun) * (size_t)z.nruns);
   put(w.off_tiny, sizeof(DevTiny) * (size_t)z.ntiny);
-  put(w.off_seeds, sizeof(uint64_t) * k);
-  put(w.off_g, sizeof(float) * 3 * k);
-  w.header = o;
-  put(w.off_sink, 256);
-  const size_t chunks = (size_t)std::max(z.reg_chunks, z.irr_chunks);
-  put(w.off_states, sizeof(uint32_t) * kMtN * (size_t)kMaxSeedsPerPass * chunks);
   w.total = o;
   return w;
+}
+
+// Caller's workspace: [sink 256 B | generator windows of one pass]
+constexpr size_t kWsStatesOff = 256;
+size_t ws_bytes_for(int chunks, int seeds_per_pass) {
+  return kWsStatesOff + sizeof(uint32_t) * kMtN * (size_t)seeds_per_pass * (size_t)std::max(chunks, 1);
 }
 
 int nsegs_total(const Layout& L) { return (int)(L.segs[0].size() + L.segs[1].size() + L.segs[2].size()); }
@@ -415,6 +419,165 @@ int timed(int which, void* stream, F&& launch) {
   return rc;
 }
 
+// ------------------------------------------------------------------ plan cache
+// The static header of a call, resident on the device.  Keyed by every input the
+// header depends on (device, CU count, each tensor's address/numel/dtype/flags/lr/wd,
+// the perturbation scales as f32, the delta base, the shard, the chunk policy); the
+// full key is compared, not only its hash.  The ZO optimizer's perturb / update calls
+// and repeated reconstructs of one model hit the cache: a call then does no host-side
+// layout work and no upload.  Bounded LRU; entries are never freed while in use
+// (launches are stream-ordered after the synchronous upload of their header).
+struct CachedPlan {
+  std::vector<uint8_t> key;
+  uint64_t hash = 0, last_use = 0;
+  void* dev = nullptr;
+  HdrLayout H;
+  HdrSizes Z;
+  size_t seg_off[3] = {0, 0, 0};
+  int nsegs[3] = {0, 0, 0};
+  int wd_mode[3] = {kModeUpdate, kModeUpdate, kModeUpdate};  // kModeUpdateWd / NoWd when uniform
+  bool have_reg = false, have_irr = false;
+};
+
+constexpr size_t kPlanCacheEntries = 32;
+std::mutex g_cache_mu;
+std::vector<CachedPlan*> g_cache;
+uint64_t g_cache_clock = 0;
+
+uint64_t fnv1a(const std::vector<uint8_t>& b) {
+  uint64_t h = 1469598103934665603ull;
+  for (uint8_t c : b) h = (h ^ c) * 1099511628211ull;
+  return h;
+}
+
+template <class T>
+void key_put(std::vector<uint8_t>& k, const T& v) {
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(&v);
+  k.insert(k.end(), p, p + sizeof(T));
+}
+
+std::vector<uint8_t> plan_key(const fks_tensor* t, int nt, const double* scales, uint64_t delta_base, int shard,
+                              int nshards, bool small) {
+  std::vector<uint8_t> k;
+  k.reserve(64 + (size_t)nt * 40);
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  key_put(k, dev);
+  key_put(k, device_cu_count());
+  key_put(k, nt);
+  key_put(k, delta_base);
+  key_put(k, shard);
+  key_put(k, nshards);
+  key_put(k, (int)small);
+  key_put(k, (int)(scales != nullptr));
+  for (int i = 0; i < nt; i++) {
+    key_put(k, t[i].data);
+    key_put(k, t[i].numel);
+    key_put(k, t[i].dtype);
+    key_put(k, t[i].flags);
+    key_put(k, t[i].lr);
+    key_put(k, t[i].wd);
+    if (scales) key_put(k, (float)scales[i]);
+  }
+  return k;
+}
+
+CachedPlan* build_plan(const fks_tensor* t, int nt, const double* scales, uint64_t delta_base, int shard,
+                       int nshards, bool small) {
+  Layout L = make_layout(t, nt, scales, delta_base);
+  const BlockRange br = shard_blocks(L.stream_len, shard, nshards);
+  clip_segments(L, br);
+  auto* C = new CachedPlan();
+  C->have_reg = nsegs_total(L) > 0;
+  C->have_irr = !L.runs.empty() || !L.tiny.empty();
+  Plan P;
+  if (C->have_reg) P = make_plan(br, small);
+  const IrrChunks IC = irregular_chunks(L);
+  std::vector<uint64_t> ipolys;
+  if (C->have_irr) jump_polys_for_blocks(IC.lo, ipolys);
+  C->Z.reg_chunks = P.nchunks;
+  C->Z.irr_chunks = (int)IC.lo.size();
+  C->Z.nsegs = nsegs_total(L);
+  C->Z.nruns = (int)L.runs.size();
+  C->Z.ntiny = (int)L.tiny.size();
+  C->H = hdr_layout(C->Z);
+  std::vector<uint8_t> host(C->H.total, 0);
+  auto put = [&](size_t off, const void* src, size_t bytes) {
+    if (bytes) std::memcpy(host.data() + off, src, bytes);
+  };
+  put(C->H.off_polys, P.polys.data(), sizeof(uint64_t) * P.polys.size());
+  put(C->H.off_cb, P.chunk_block.data(), sizeof(int64_t) * P.chunk_block.size());
+  put(C->H.off_ipolys, ipolys.data(), sizeof(uint64_t) * ipolys.size());
+  put(C->H.off_ilo, IC.lo.data(), sizeof(int64_t) * IC.lo.size());
+  put(C->H.off_ihi, IC.hi.data(), sizeof(int64_t) * IC.hi.size());
+  size_t so = C->H.off_segs;
+  for (int d = 0; d < 3; d++) {
+    C->seg_off[d] = so;
+    C->nsegs[d] = (int)L.segs[d].size();
+    put(so, L.segs[d].data(), sizeof(DevSeg) * L.segs[d].size());
+    so += sizeof(DevSeg) * L.segs[d].size();
+    size_t nwd = 0;
+    for (const DevSeg& sg : L.segs[d]) nwd += (sg.flags & FKS_HAS_WD) ? 1 : 0;
+    if (!L.segs[d].empty() && nwd == L.segs[d].size()) C->wd_mode[d] = kModeUpdateWd;
+    else if (!L.segs[d].empty() && nwd == 0) C->wd_mode[d] = kModeUpdateNoWd;
+  }
+  put(C->H.off_runs, L.runs.data(), sizeof(DevRun) * L.runs.size());
+  put(C->H.off_tiny, L.tiny.data(), sizeof(DevTiny) * L.tiny.size());
+  hipError_t e = hipMalloc(&C->dev, std::max<size_t>(C->H.total, 256));
+  if (e != hipSuccess) {
+    delete C;
+    throw Error(-FKS_ENOMEM, std::string("plan cache hipMalloc: ") + hipGetErrorString(e));
+  }
+  // synchronous: every later launch on any stream finds the header in place
+  e = hipMemcpy(C->dev, host.data(), C->H.total, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(C->dev);
+    delete C;
+    throw Error(-FKS_EHIP, std::string("plan upload: ") + hipGetErrorString(e));
+  }
+  return C;
+}
+
+// The cached plan for these inputs (built and uploaded on a miss).  The caller holds
+// g_cache_mu for as long as it uses the entry (run() holds it across its launches).
+// Entries evicted from the LRU are freed after a device synchronisation, so no
+// in-flight launch can still read them.
+CachedPlan* get_plan(const fks_tensor* t, int nt, const double* scales, uint64_t delta_base, int shard, int nshards,
+                     bool small) {
+  std::vector<uint8_t> key = plan_key(t, nt, scales, delta_base, shard, nshards, small);
+  const uint64_t h = fnv1a(key);
+  for (CachedPlan* C : g_cache) {
+    if (C->hash == h && C->key == key) {
+      C->last_use = ++g_cache_clock;
+      return C;
+    }
+  }
+  CachedPlan* C = build_plan(t, nt, scales, delta_base, shard, nshards, small);
+  C->key = std::move(key);
+  C->hash = h;
+  C->last_use = ++g_cache_clock;
+  if (g_cache.size() >= kPlanCacheEntries) {
+    auto victim = std::min_element(g_cache.begin(), g_cache.end(),
+                                   [](const CachedPlan* a, const CachedPlan* b) { return a->last_use < b->last_use; });
+    (void)hipDeviceSynchronize();
+    (void)hipFree((*victim)->dev);
+    delete *victim;
+    g_cache.erase(victim);
+  }
+  g_cache.push_back(C);
+  return C;
+}
+
+void clear_plan_cache() {
+  std::lock_guard<std::mutex> lk(g_cache_mu);
+  if (!g_cache.empty()) (void)hipDeviceSynchronize();
+  for (CachedPlan* C : g_cache) {
+    (void)hipFree(C->dev);
+    delete C;
+  }
+  g_cache.clear();
+}
+
 void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* values, int k, int value_kind, int mode,
          void* workspace, size_t ws_bytes, void* stream, const double* tensor_scales = nullptr, int shard = 0,
          int nshards = 1, uint64_t delta_base = 0) {
@@ -423,116 +586,73 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
   if (k < 0 || (k > 0 && (!seeds || !values))) throw Error(-FKS_EINVAL, "bad seed/value arrays");
   if (value_kind != FKS_VALUE_SCALAR && value_kind != FKS_VALUE_TENSOR)
     throw Error(-FKS_EINVAL, "bad value_kind");
-  Layout L = make_layout(t, nt, tensor_scales, delta_base);
-  const BlockRange br = shard_blocks(L.stream_len, shard, nshards);
-  clip_segments(L, br);
-  const bool have_reg = nsegs_total(L) > 0, have_irr = !L.runs.empty() || !L.tiny.empty();
-  if (k == 0 || (!have_reg && !have_irr)) return;
-  Plan P;
-  if (have_reg) P = make_plan(br);
-  const IrrChunks IC = irregular_chunks(L);
-  std::vector<uint64_t> ipolys;
-  if (have_irr) jump_polys_for_blocks(IC.lo, ipolys);
-  WsSizes z;
-  z.reg_chunks = P.nchunks;
-  z.irr_chunks = (int)IC.lo.size();
-  z.nsegs = nsegs_total(L);
-  z.nruns = (int)L.runs.size();
-  z.ntiny = (int)L.tiny.size();
-  z.k = k;
-  const WsLayout W = ws_layout(z);
-  if (!workspace || ws_bytes < W.total)
-    throw Error(-FKS_EINVAL, "workspace too small: need " + std::to_string(W.total) + " bytes, got " +
+  if (k == 0 || nt == 0) return;
+  const bool small = k <= kSmallK;
+  std::lock_guard<std::mutex> lk(g_cache_mu);  // no eviction while this call uses its entry
+  const CachedPlan* C = get_plan(t, nt, tensor_scales, delta_base, shard, nshards, small);
+  if (!C->have_reg && !C->have_irr) return;
+  const int per_pass = small ? kSmallK : kMaxSeedsPerPass;
+  const size_t need = ws_bytes_for(std::max(C->Z.reg_chunks, C->Z.irr_chunks), std::min(per_pass, k));
+  if (!workspace || ws_bytes < need)
+    throw Error(-FKS_EINVAL, "workspace too small: need " + std::to_string(need) + " bytes, got " +
                                  std::to_string(ws_bytes));
-  // header upload (one async H2D copy from a per-thread host buffer; a pageable
-  // source is staged before hipMemcpyAsync returns, so the buffer is reusable)
-  thread_local std::vector<uint8_t> host;
-  host.assign(W.header, 0);
-  auto put = [&](size_t off, const void* src, size_t bytes) {
-    if (bytes) std::memcpy(host.data() + off, src, bytes);
-  };
-  put(W.off_polys, P.polys.data(), sizeof(uint64_t) * P.polys.size());
-  put(W.off_cb, P.chunk_block.data(), sizeof(int64_t) * P.chunk_block.size());
-  put(W.off_ipolys, ipolys.data(), sizeof(uint64_t) * ipolys.size());
-  put(W.off_ilo, IC.lo.data(), sizeof(int64_t) * IC.lo.size());
-  put(W.off_ihi, IC.hi.data(), sizeof(int64_t) * IC.hi.size());
-  size_t so = W.off_segs;
-  size_t seg_off[3];
-  for (int d = 0; d < 3; d++) {
-    seg_off[d] = so;
-    put(so, L.segs[d].data(), sizeof(DevSeg) * L.segs[d].size());
-    so += sizeof(DevSeg) * L.segs[d].size();
-  }
-  put(W.off_runs, L.runs.data(), sizeof(DevRun) * L.runs.size());
-  put(W.off_tiny, L.tiny.data(), sizeof(DevTiny) * L.tiny.size());
-  put(W.off_seeds, seeds, sizeof(uint64_t) * (size_t)k);
-  float* gh = reinterpret_cast<float*>(host.data() + W.off_g);
-  for (int d = 0; d < 3; d++)
-    for (int s = 0; s < k; s++)
-      gh[(size_t)d * k + s] = value_kind == FKS_VALUE_TENSOR ? round_to_dtype(values[s], d) : (float)values[s];
-  uint8_t* ws = static_cast<uint8_t*>(workspace);
-  hipError_t e = hipMemcpyAsync(ws, host.data(), W.header, hipMemcpyHostToDevice, (hipStream_t)stream);
-  if (e != hipSuccess) throw Error(-FKS_EHIP, std::string("hipMemcpyAsync: ") + hipGetErrorString(e));
-
   auto check = [](int rc, const char* what) {
     if (rc) throw Error(rc < 0 ? rc : -FKS_EHIP, std::string(what) + " launch: " +
                                                    (rc > 0 ? hipGetErrorString((hipError_t)rc) : "unsupported"));
   };
-  uint32_t* states = reinterpret_cast<uint32_t*>(ws + W.off_states);
-  const uint64_t* dseeds = reinterpret_cast<const uint64_t*>(ws + W.off_seeds);
-  const float* dg = reinterpret_cast<const float*>(ws + W.off_g);
+  uint8_t* ws = static_cast<uint8_t*>(workspace);
+  const uint8_t* hdr = static_cast<const uint8_t*>(C->dev);
+  uint32_t* states = reinterpret_cast<uint32_t*>(ws + kWsStatesOff);
+  auto gval = [&](int s, int d) -> float {
+    return value_kind == FKS_VALUE_TENSOR ? round_to_dtype(values[s], d) : (float)values[s];
+  };
   for (int s0 = 0; s0 < k; s0 += kMaxSeedsPerPass) {
     const int nb = std::min(kMaxSeedsPerPass, k - s0);
-    if (have_reg) {
+    if (C->have_reg) {
       JumpArgs ja{};
-      ja.seeds = dseeds + s0;
-      ja.polys = reinterpret_cast<const uint64_t*>(ws + W.off_polys);
-      ja.chunk_block = reinterpret_cast<const int64_t*>(ws + W.off_cb);
+      for (int j = 0; j < nb; j++) ja.seeds[j] = seeds[s0 + j];
+      ja.polys = reinterpret_cast<const uint64_t*>(hdr + C->H.off_polys);
+      ja.chunk_block = reinterpret_cast<const int64_t*>(hdr + C->H.off_cb);
       ja.states = states;
-      ja.nchunks = P.nchunks;
-      ja.chunks_per_wg = std::max(1, std::min(32, P.nchunks));  // 2 jumps per wave (16 waves)
+      ja.nchunks = C->Z.reg_chunks;
+      // one chunk per wave when few seeds would leave most CUs idle
+      ja.chunks_per_wg = std::max(1, std::min(nb * C->Z.reg_chunks >= 4096 ? 32 : 16, C->Z.reg_chunks));
       check(timed(1, stream, [&] { return launch_jump(ja, nb, stream); }), "fks_jump_kernel");
       for (int d = 0; d < 3; d++) {
-        if (L.segs[d].empty()) continue;
+        if (!C->nsegs[d]) continue;
         ApplyArgs aa{};
         aa.states = states;
-        aa.g = dg + (size_t)d * k + s0;
-        aa.segs = reinterpret_cast<const DevSeg*>(ws + seg_off[d]);
+        for (int j = 0; j < nb; j++) aa.g[j] = gval(s0 + j, d);
+        aa.segs = reinterpret_cast<const DevSeg*>(hdr + C->seg_off[d]);
         aa.chunk_block = ja.chunk_block;
-        aa.sink = reinterpret_cast<uint64_t*>(ws + W.off_sink);
-        aa.nsegs = (int)L.segs[d].size();
-        aa.nchunks = P.nchunks;
+        aa.sink = reinterpret_cast<uint64_t*>(ws);
+        aa.nsegs = C->nsegs[d];
+        aa.nchunks = C->Z.reg_chunks;
         aa.nseeds = nb;
-        aa.mode = mode;
-        if (mode == kModeUpdate) {  // specialise the weight-decay select away when uniform
-          size_t nwd = 0;
-          for (const DevSeg& sg : L.segs[d]) nwd += (sg.flags & FKS_HAS_WD) ? 1 : 0;
-          if (nwd == L.segs[d].size()) aa.mode = kModeUpdateWd;
-          else if (nwd == 0) aa.mode = kModeUpdateNoWd;
-        }
+        aa.mode = mode == kModeUpdate ? C->wd_mode[d] : mode;  // weight-decay select specialised away
         check(timed(0, stream, [&] { return launch_apply(d, aa, stream); }), "fks_apply_kernel");
       }
     }
-    if (have_irr) {
+    if (C->have_irr) {
       JumpArgs ja{};
-      ja.seeds = dseeds + s0;
-      ja.polys = reinterpret_cast<const uint64_t*>(ws + W.off_ipolys);
-      ja.chunk_block = reinterpret_cast<const int64_t*>(ws + W.off_ilo);
+      for (int j = 0; j < nb; j++) ja.seeds[j] = seeds[s0 + j];
+      ja.polys = reinterpret_cast<const uint64_t*>(hdr + C->H.off_ipolys);
+      ja.chunk_block = reinterpret_cast<const int64_t*>(hdr + C->H.off_ilo);
       ja.states = states;
-      ja.nchunks = z.irr_chunks;
-      ja.chunks_per_wg = std::max(1, std::min(32, z.irr_chunks));
+      ja.nchunks = C->Z.irr_chunks;
+      ja.chunks_per_wg = std::max(1, std::min(32, C->Z.irr_chunks));
       check(timed(1, stream, [&] { return launch_jump(ja, nb, stream); }), "fks_jump_kernel");
       IrrArgs ia{};
       ia.states = states;
-      ia.g = dg + s0;
-      ia.gstride = k;
-      ia.runs = reinterpret_cast<const DevRun*>(ws + W.off_runs);
-      ia.tiny = reinterpret_cast<const DevTiny*>(ws + W.off_tiny);
+      for (int d = 0; d < 3; d++)
+        for (int j = 0; j < nb; j++) ia.g[d][j] = gval(s0 + j, d);
+      ia.runs = reinterpret_cast<const DevRun*>(hdr + C->H.off_runs);
+      ia.tiny = reinterpret_cast<const DevTiny*>(hdr + C->H.off_tiny);
       ia.chunk_lo = ja.chunk_block;
-      ia.chunk_hi = reinterpret_cast<const int64_t*>(ws + W.off_ihi);
-      ia.nruns = z.nruns;
-      ia.ntiny = z.ntiny;
-      ia.nchunks = z.irr_chunks;
+      ia.chunk_hi = reinterpret_cast<const int64_t*>(hdr + C->H.off_ihi);
+      ia.nruns = C->Z.nruns;
+      ia.ntiny = C->Z.ntiny;
+      ia.nchunks = C->Z.irr_chunks;
       ia.nseeds = nb;
       ia.mode = mode;
       check(timed(0, stream, [&] { return launch_irregular(ia, stream); }), "fks_irregular_kernel");
@@ -633,19 +753,14 @@ int fks_delta_apply(const fks_tensor* t, int32_t nt, const float* delta, const d
 namespace fks {
 namespace {
 size_t workspace_total(const fks_tensor* t, int nt, int k, uint64_t delta_base) {
-  {
-    const Layout L = make_layout(t, nt, nullptr, delta_base);
-    // upper bounds over every shard count: a shard never needs more chunks, segments,
-    // runs or single elements than the whole stream
-    WsSizes z;
-    if (nsegs_total(L)) z.reg_chunks = plan_nchunks(shard_blocks(L.stream_len, 0, 1).hi);
-    if (!L.runs.empty() || !L.tiny.empty()) z.irr_chunks = plan_nchunks(irregular_covered_blocks(L));
-    z.nsegs = nsegs_total(L);
-    z.nruns = (int)L.runs.size();
-    z.ntiny = (int)L.tiny.size();
-    z.k = std::max(k, 1);
-    return ws_layout(z).total;
-  }
+  // upper bound over every shard count: a shard never needs more chunks than the whole
+  // stream; the header itself lives in the plan cache, not in the workspace
+  const Layout L = make_layout(t, nt, nullptr, delta_base);
+  const bool small = k <= kSmallK;
+  int chunks = 0;
+  if (nsegs_total(L)) chunks = plan_nchunks(shard_blocks(L.stream_len, 0, 1).hi, small);
+  if (!L.runs.empty() || !L.tiny.empty()) chunks = std::max(chunks, plan_nchunks(irregular_covered_blocks(L)));
+  return ws_bytes_for(chunks, std::max(1, std::min(k, small ? kSmallK : kMaxSeedsPerPass)));
 }
 }  // namespace
 }  // namespace fks
@@ -749,6 +864,10 @@ int fks_normal(const fks_tensor* t, int32_t nt, uint64_t seed, void* workspace, 
     const double v = 0.0;
     run(t, nt, &seed, &v, 1, FKS_VALUE_SCALAR, kModeWriteZ, workspace, ws_bytes, stream);
   });
+}
+
+int fks_plan_cache_clear(void) {
+  return guarded([&] { clear_plan_cache(); });
 }
 
 const char* fks_last_error(void) { return g_last_error.c_str(); }

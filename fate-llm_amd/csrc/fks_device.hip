@@ -848,8 +848,10 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
       if constexpr (FULL) {
         pair_all<DT, MODE, kMaxSeedsPerPass>(lds, st_off, gk, sl.lr, sl.wd, sl.wdf != 0, sl.ps, p1, p2);
       } else {
+        // a.g[k] straight from the kernel-argument segment (one s_load per seed): a
+        // dynamically indexed gk[] would be copied to VGPRs and indexed per seed
         for (int k = 0; k < nseeds; k++)
-          pair_one<DT, MODE>(lds, st_off, k, gk[k], sl.lr, sl.wd, sl.wdf != 0, sl.ps, p1, p2);
+          pair_one<DT, MODE>(lds, st_off, k, a.g[k], sl.lr, sl.wd, sl.wdf != 0, sl.ps, p1, p2);
       }
       const uint32_t b1v = ST::bits(p1), b2v = ST::bits(p2);
       const uint32_t back = swap_adjacent(odd ? b1v : b2v);  // even gets partner's p1, odd partner's p2
@@ -955,7 +957,7 @@ __device__ __forceinline__ void irr_run_lane(const uint8_t* lds, const uint32_t*
     if (on2) p2 = TR::load(R.ptr, e1 + 8);
   }
   const bool has_wd = (R.flags & FKS_HAS_WD) != 0;
-  const float* g = a.g + (size_t)DT * a.gstride;
+  const float* g = a.g[DT];
   for (int k = 0; k < a.nseeds; k++) {
     float z1, z2;
     irr_z_pair<DT>(lds, win_word(win, k, w1), win_word(win, k, w1 + 8), z1, z2);
@@ -977,7 +979,7 @@ __device__ __forceinline__ void irr_tiny_lane(const uint32_t* win, const IrrArgs
   float p = MODE != kModeWriteZ ? TR::load(T.ptr, 0) : 0.0f;
   const bool has_wd = (T.flags & FKS_HAS_WD) != 0;
   const bool sin_half = (T.flags & kTinySin) != 0;
-  const float* g = a.g + (size_t)DT * a.gstride;
+  const float* g = a.g[DT];
   for (int k = 0; k < a.nseeds; k++) {
     const double u1 = u53(mt_temper(win_word(win, k, w)), mt_temper(win_word(win, k, w + 1)));
     const double u2 = u53(mt_temper(win_word(win, k, w + 2)), mt_temper(win_word(win, k, w + 3)));
@@ -1162,11 +1164,13 @@ int launch_jump(const JumpArgs& a, int nseeds, void* stream) {
 
 template <int DT, int MODE, bool FULL>
 static int launch_apply_f(const ApplyArgs& a, void* stream) {
-  const size_t lds = apply_lds_bytes();
+  // a partial pass allocates only its own windows (+1 spare: the twist's last-phase lanes
+  // read past a window), so calls of few seeds fit more workgroups per CU
+  const size_t lds = FULL ? apply_lds_bytes() : (size_t)kLdsTabBytes + (size_t)(a.nseeds + 1) * kWinBytes;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fks_apply_kernel<DT, MODE, FULL>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)apply_lds_bytes());
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
@@ -1182,6 +1186,7 @@ static int launch_apply_t(const ApplyArgs& a, void* stream) {
 }
 
 int launch_apply(int dtype, const ApplyArgs& a, void* stream) {
+  if (a.nseeds < 1 || a.nseeds > kMaxSeedsPerPass || a.nchunks < 1) return -FKS_EINVAL;
   if (dtype == FKS_BF16) {
     int e = ensure_tables();
     if (e) return e;

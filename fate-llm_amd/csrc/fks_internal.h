@@ -90,6 +90,9 @@ constexpr int kApplyThreads = 320;  // 312 Box-Muller pairs per 624-word block +
 constexpr int kApplyWgPerCu = FKS_APPLY_WG_PER_CU;  // resident apply workgroups per CU (LDS-limited)
 // MT windows resident in LDS per workgroup: (seeds + 1 spare) x 2496 B + 4 KB tables <= 160 KB / WGs
 constexpr int kMaxSeedsPerPass = (160 * 1024 / kApplyWgPerCu - 4096) / 2496 - 1;  // tables: <= 4 KB
+// calls of at most kSmallK seeds run one pass over kSmallWgPerCu workgroups per CU
+constexpr int kSmallK = 4;
+constexpr int kSmallWgPerCu = 4;  // VGPR-limited (partial-pass variants: <= 96 VGPRs, 5 waves/SIMD)
 constexpr int kJumpThreads = 1024;  // 16 waves, one chunk's jump per wave at a time
 constexpr int kJumpXLen = 19937 + 624;  // x[0..20560]: y[i + w] = x[i + w + 1], i < 19937, w < 624
 
@@ -104,9 +107,12 @@ enum ApplyMode : int {
   kModeDelta = 6
 };
 
+// Per-pass seeds and multipliers travel BY VALUE in the kernel arguments: a call
+// uploads nothing per pass, and the static header (chunk table, jump polynomials,
+// descriptors) is cached on the device across calls (fks_capi.cpp, PlanCache).
 struct ApplyArgs {
   const uint32_t* states;       // [nseeds][nchunks][624] generator windows at chunk starts
-  const float* g;               // [nseeds] update multiplier (mode 0); perturb scales ride in DevSeg::lr
+  float g[kMaxSeedsPerPass];    // update multiplier per seed (mode 0) / delta coefficient
   const DevSeg* segs;           // regular segments of this launch's dtype, sorted by start
   const int64_t* chunk_block;   // [nchunks + 1] first MT block of each chunk
   uint64_t* sink;               // 16 bytes of workspace: loads/stores of idle lanes
@@ -118,12 +124,11 @@ struct ApplyArgs {
 
 struct IrrArgs {
   const uint32_t* states;       // [nseeds][nchunks][624]
-  const float* g;               // [3][gstride]: per-dtype multipliers of this pass's seeds
+  float g[3][kMaxSeedsPerPass]; // per-dtype multipliers of this pass's seeds
   const DevRun* runs;           // sorted by start (disjoint)
   const DevTiny* tiny;          // sorted by word
   const int64_t* chunk_lo;      // [nchunks] chunk c twists MT blocks [chunk_lo[c], chunk_hi[c])
   const int64_t* chunk_hi;
-  int64_t gstride;
   int32_t nruns;
   int32_t ntiny;
   int32_t nchunks;
@@ -132,7 +137,7 @@ struct IrrArgs {
 };
 
 struct JumpArgs {
-  const uint64_t* seeds;        // [nseeds]
+  uint64_t seeds[kMaxSeedsPerPass];
   const uint64_t* polys;        // [nchunks][312] t^(624*b-1) mod phi (unused for b == 0)
   const int64_t* chunk_block;   // [nchunks + 1]
   uint32_t* states;             // [nseeds][nchunks][624]

@@ -114,6 +114,15 @@ int fks_stream_length(const fks_tensor* t, int32_t nt, int64_t* words);
 int fks_profile_begin(void);
 int fks_profile_end(double* apply_ms, int64_t* n_apply, double* jump_ms, int64_t* n_jump);
 
+/* Every call's static header (MT-block chunk table, jump polynomials, segment / run /
+ * element descriptors) is built on the host and uploaded ONCE per distinct tensor list
+ * (addresses, sizes, dtypes, flags, lr, wd, perturbation scales, shard), then kept on
+ * the device in a bounded LRU plan cache: repeated calls over the same parameters (the
+ * optimizer's perturb / update calls, repeated reconstructs) do no host-side layout
+ * work and no upload.  fks_plan_cache_clear synchronises the device and frees every
+ * cached header (e.g. before freeing the parameters' memory pool). */
+int fks_plan_cache_clear(void);
+
 /* torch.manual_seed(seed); for every tensor i in order: p = p + scales[i]*z, where
  * scales[i] = scaling_factor*eps of the tensor's group, computed in double by the
  * caller (optimizer.py:167,173).  Tensors with requires_grad=False draw nothing in
