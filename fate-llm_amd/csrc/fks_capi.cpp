@@ -325,11 +325,12 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // per-pass seeds and multipliers travel by value in the kernel arguments.
 struct HdrSizes {
   int reg_chunks = 0, irr_chunks = 0, nsegs = 0, nruns = 0, ntiny = 0;
+  int bs_chunks = 0;  // the bf16 slice kernel's own chunk plan (0: not used)
 };
 
 struct HdrLayout {
   size_t off_polys = 0, off_cb = 0, off_ipolys = 0, off_ilo = 0, off_ihi = 0, off_segs = 0, off_runs = 0,
-         off_tiny = 0;
+         off_tiny = 0, off_bs_polys = 0, off_bs_cb = 0;
   size_t total = 0;
 };
 
@@ -345,6 +346,8 @@ HdrLayout hdr_layout(const HdrSizes& z) {
   put(w.off_segs, sizeof(DevSeg) * (size_t)z.nsegs);
   put(w.off_runs, sizeof(DevRun) * (size_t)z.nruns);
   put(w.off_tiny, sizeof(DevTiny) * (size_t)z.ntiny);
+  put(w.off_bs_polys, sizeof(uint64_t) * 312 * (size_t)z.bs_chunks);
+  put(w.off_bs_cb, sizeof(int64_t) * ((size_t)z.bs_chunks + 1));
   w.total = o;
   return w;
 }
@@ -353,6 +356,19 @@ HdrLayout hdr_layout(const HdrSizes& z) {
 constexpr size_t kWsStatesOff = 256;
 size_t ws_bytes_for(int chunks, int seeds_per_pass) {
   return kWsStatesOff + sizeof(uint32_t) * kMtN * (size_t)seeds_per_pass * (size_t)std::max(chunks, 1);
+}
+
+// the slice kernel's plan: kBsChunksPerWg chunks per workgroup, one workgroup per CU
+int bs_nchunks(int64_t nblocks) {
+  const int64_t wgs = std::max<int64_t>(1, std::min<int64_t>(device_cu_count(), (nblocks + 1) / 2));
+  return (int)(kBsChunksPerWg * wgs);
+}
+
+Plan make_plan_n(BlockRange r, int nchunks) {
+  const int64_t nblocks = std::max<int64_t>(1, r.hi - r.lo);
+  std::vector<int64_t> cb((size_t)nchunks + 1);
+  for (int c = 0; c <= nchunks; c++) cb[(size_t)c] = r.lo + (int64_t)((__int128)nblocks * c / nchunks);
+  return plan_from_blocks(std::move(cb));
 }
 
 int nsegs_total(const Layout& L) { return (int)(L.segs[0].size() + L.segs[1].size() + L.segs[2].size()); }
@@ -437,6 +453,7 @@ struct CachedPlan {
   int nsegs[3] = {0, 0, 0};
   int wd_mode[3] = {kModeUpdate, kModeUpdate, kModeUpdate};  // kModeUpdateWd / NoWd when uniform
   bool have_reg = false, have_irr = false;
+  bool have_bs = false;  // bf16 fast segments with their slice-kernel plan (non-small calls)
 };
 
 constexpr size_t kPlanCacheEntries = 32;
@@ -492,6 +509,9 @@ CachedPlan* build_plan(const fks_tensor* t, int nt, const double* scales, uint64
   C->have_irr = !L.runs.empty() || !L.tiny.empty();
   Plan P;
   if (C->have_reg) P = make_plan(br, small);
+  Plan BP;
+  C->have_bs = !small && !L.segs[FKS_BF16].empty();
+  if (C->have_bs) BP = make_plan_n(br, bs_nchunks(br.hi - br.lo));
   const IrrChunks IC = irregular_chunks(L);
   std::vector<uint64_t> ipolys;
   if (C->have_irr) jump_polys_for_blocks(IC.lo, ipolys);
@@ -500,6 +520,7 @@ CachedPlan* build_plan(const fks_tensor* t, int nt, const double* scales, uint64
   C->Z.nsegs = nsegs_total(L);
   C->Z.nruns = (int)L.runs.size();
   C->Z.ntiny = (int)L.tiny.size();
+  C->Z.bs_chunks = BP.nchunks;
   C->H = hdr_layout(C->Z);
   std::vector<uint8_t> host(C->H.total, 0);
   auto put = [&](size_t off, const void* src, size_t bytes) {
@@ -510,6 +531,8 @@ CachedPlan* build_plan(const fks_tensor* t, int nt, const double* scales, uint64
   put(C->H.off_ipolys, ipolys.data(), sizeof(uint64_t) * ipolys.size());
   put(C->H.off_ilo, IC.lo.data(), sizeof(int64_t) * IC.lo.size());
   put(C->H.off_ihi, IC.hi.data(), sizeof(int64_t) * IC.hi.size());
+  put(C->H.off_bs_polys, BP.polys.data(), sizeof(uint64_t) * BP.polys.size());
+  put(C->H.off_bs_cb, BP.chunk_block.data(), sizeof(int64_t) * BP.chunk_block.size());
   size_t so = C->H.off_segs;
   for (int d = 0; d < 3; d++) {
     C->seg_off[d] = so;
@@ -592,7 +615,11 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
   const CachedPlan* C = get_plan(t, nt, tensor_scales, delta_base, shard, nshards, small);
   if (!C->have_reg && !C->have_irr) return;
   const int per_pass = small ? kSmallK : kMaxSeedsPerPass;
-  const size_t need = ws_bytes_for(std::max(C->Z.reg_chunks, C->Z.irr_chunks), std::min(per_pass, k));
+  // bf16 fast segments of a reconstruct (or delta accumulation) of more than one
+  // 19-seed pass go to the bit-sliced slice kernel, 32 seeds per pass
+  const bool use_bs = C->have_bs && k >= kBsMinSeeds && (mode == kModeUpdate || mode == kModeDelta);
+  size_t need = ws_bytes_for(std::max(C->Z.reg_chunks, C->Z.irr_chunks), std::min(per_pass, k));
+  if (use_bs) need = std::max(need, ws_bytes_for(C->Z.bs_chunks, std::min(kBsSeeds, k)));
   if (!workspace || ws_bytes < need)
     throw Error(-FKS_EINVAL, "workspace too small: need " + std::to_string(need) + " bytes, got " +
                                  std::to_string(ws_bytes));
@@ -606,9 +633,36 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
   auto gval = [&](int s, int d) -> float {
     return value_kind == FKS_VALUE_TENSOR ? round_to_dtype(values[s], d) : (float)values[s];
   };
+  if (use_bs) {
+    for (int s0 = 0; s0 < k; s0 += kBsSeeds) {
+      const int nb = std::min(kBsSeeds, k - s0);
+      JumpArgs ja{};
+      for (int j = 0; j < nb; j++) ja.seeds[j] = seeds[s0 + j];
+      ja.polys = reinterpret_cast<const uint64_t*>(hdr + C->H.off_bs_polys);
+      ja.chunk_block = reinterpret_cast<const int64_t*>(hdr + C->H.off_bs_cb);
+      ja.states = states;
+      ja.nchunks = C->Z.bs_chunks;
+      ja.chunks_per_wg = std::max(1, std::min(nb * C->Z.bs_chunks >= 4096 ? 32 : 16, C->Z.bs_chunks));
+      check(timed(1, stream, [&] { return launch_jump(ja, nb, stream); }), "fks_jump_kernel");
+      ApplyBsArgs ba{};
+      ba.states = states;
+      for (int j = 0; j < nb; j++) ba.g[j] = gval(s0 + j, FKS_BF16);
+      ba.segs = reinterpret_cast<const DevSeg*>(hdr + C->seg_off[FKS_BF16]);
+      ba.chunk_block = ja.chunk_block;
+      ba.sink = reinterpret_cast<uint64_t*>(ws);
+      ba.nsegs = C->nsegs[FKS_BF16];
+      ba.nchunks = C->Z.bs_chunks;
+      ba.nseeds = nb;
+      ba.mode = mode == kModeUpdate ? C->wd_mode[FKS_BF16] : mode;
+      check(timed(0, stream, [&] { return launch_apply_bs(ba, stream); }), "fks_apply_bs_kernel");
+    }
+  }
+  // the 19-seed kernels: every other regular dtype (all of them without the slice kernel)
+  bool reg_rest = false;
+  for (int d = 0; d < 3; d++) reg_rest = reg_rest || (C->nsegs[d] && !(use_bs && d == FKS_BF16));
   for (int s0 = 0; s0 < k; s0 += kMaxSeedsPerPass) {
     const int nb = std::min(kMaxSeedsPerPass, k - s0);
-    if (C->have_reg) {
+    if (reg_rest) {
       JumpArgs ja{};
       for (int j = 0; j < nb; j++) ja.seeds[j] = seeds[s0 + j];
       ja.polys = reinterpret_cast<const uint64_t*>(hdr + C->H.off_polys);
@@ -619,7 +673,7 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
       ja.chunks_per_wg = std::max(1, std::min(nb * C->Z.reg_chunks >= 4096 ? 32 : 16, C->Z.reg_chunks));
       check(timed(1, stream, [&] { return launch_jump(ja, nb, stream); }), "fks_jump_kernel");
       for (int d = 0; d < 3; d++) {
-        if (!C->nsegs[d]) continue;
+        if (!C->nsegs[d] || (use_bs && d == FKS_BF16)) continue;
         ApplyArgs aa{};
         aa.states = states;
         for (int j = 0; j < nb; j++) aa.g[j] = gval(s0 + j, d);
@@ -758,9 +812,13 @@ size_t workspace_total(const fks_tensor* t, int nt, int k, uint64_t delta_base) 
   const Layout L = make_layout(t, nt, nullptr, delta_base);
   const bool small = k <= kSmallK;
   int chunks = 0;
-  if (nsegs_total(L)) chunks = plan_nchunks(shard_blocks(L.stream_len, 0, 1).hi, small);
+  const int64_t nblocks = shard_blocks(L.stream_len, 0, 1).hi;
+  if (nsegs_total(L)) chunks = plan_nchunks(nblocks, small);
   if (!L.runs.empty() || !L.tiny.empty()) chunks = std::max(chunks, plan_nchunks(irregular_covered_blocks(L)));
-  return ws_bytes_for(chunks, std::max(1, std::min(k, small ? kSmallK : kMaxSeedsPerPass)));
+  size_t bytes = ws_bytes_for(chunks, std::max(1, std::min(k, small ? kSmallK : kMaxSeedsPerPass)));
+  if (!small && k >= kBsMinSeeds && !L.segs[FKS_BF16].empty())  // the slice kernel's windows
+    bytes = std::max(bytes, ws_bytes_for(bs_nchunks(nblocks), std::min(k, kBsSeeds)));
+  return bytes;
 }
 }  // namespace
 }  // namespace fks

@@ -19,6 +19,7 @@
 #include <hip/hip_bf16.h>
 
 #include "fks_internal.h"
+#include "fks_bitslice.h"
 
 #ifndef FKS_DIAG
 #define FKS_DIAG 0  // diagnostic builds only (make diag): timing variants with wrong results
@@ -883,6 +884,277 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
 #endif
 }
 
+// ------------------------------------------------------------------ bf16 slice kernel
+// fks_apply_bs_kernel<MODE>: the bf16 fast segments of a reconstruct, 32 seeds per
+// pass, generator state BIT-SLICED (fks_bitslice.h).  One workgroup per CU, two
+// independent halves (chunks 2w and 2w+1 of the stream) sharing the LDS tables:
+//   * waves 0..4 of a half: thread q < 312 owns Box-Muller pair q of every block, as in
+//     fks_apply_kernel; per block it reads state rows j1 and j1+8 (32 planes each),
+//     tempers their low bytes (temper_low8), transposes them to one byte per seed
+//     (transpose8), and runs the 32-seed update chain of its two parameters in order;
+//   * wave 5 of a half twists the half's state in place, block b -> b+1, while the
+//     pair waves run block b's chain: 10 rounds of 64 rows, all reads of a round
+//     before its writes (one wave: LDS operations complete in order, so no barrier).
+// Per block: barrier (state holds block b) -> pair waves read + temper their rows ->
+// barrier (rows consumed) -> twist || chain.
+// LDS: [R f32 x 256 | (C,S) f32x2 x 256 | state half 0 | state half 1]; a half's state
+// is 8 CHUNK arrays (planes 4q..4q+3 of all 624 rows, 16 B per row): consecutive rows
+// are consecutive 16 B, so the twist wave's row reads and writes are bank-conflict
+// free; the pair waves read row j1 first where (q >> 4) is even and row j1+8 first
+// where it is odd, which makes every 16-lane ds_read_b128 group hit 16 distinct rows
+// mod 16 (conflict free as well).
+constexpr int kBsChunkBytes = kMtN * 16;               // 9,984
+constexpr int kBsStateBytes = 8 * kBsChunkBytes;       // 79,872
+constexpr int kBsTabBytes = 256 * 4 + 256 * 8;         // 3,072
+constexpr int kBsLdsBytes = kBsTabBytes + 2 * kBsStateBytes;  // 162,816 <= 163,840
+static_assert(kBsLdsBytes <= 163840, "slice kernel LDS");
+
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4_t lds_u4_t;
+__device__ __forceinline__ u32x4_t lds_u4(uint32_t off) { return *(const lds_u4_t*)(size_t)off; }
+__device__ __forceinline__ void lds_st4(uint32_t off, u32x4_t v) { *(lds_u4_t*)(size_t)off = v; }
+
+// the 32 planes of row i (row byte address ra = state base + 16 i)
+__device__ __forceinline__ void bs_load_row(uint32_t ra, uint32_t (&x)[32]) {
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const u32x4_t v = lds_u4(ra + q * kBsChunkBytes);
+    x[4 * q] = v.x;
+    x[4 * q + 1] = v.y;
+    x[4 * q + 2] = v.z;
+    x[4 * q + 3] = v.w;
+  }
+}
+__device__ __forceinline__ void bs_store_row(uint32_t ra, const uint32_t (&x)[32]) {
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const u32x4_t v = {x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]};
+    lds_st4(ra + q * kBsChunkBytes, v);
+  }
+}
+
+// row addresses of twist round r for this lane: i = 64 r + lane; V = row i+1 (row 0 for
+// i = 623), M = row i+397 (i < 227) or i-227; lanes with i >= 624 read row 0 and do
+// not store.
+__device__ __forceinline__ void bs_round_rows(uint32_t sbase, int r, int lane, uint32_t& av, uint32_t& am) {
+  const int i = 64 * r + lane;
+  const int iv = i + 1 < kMtN ? i + 1 : 0;
+  const int im = i < kMtN - kMtM ? i + kMtM : (i < kMtN ? i - (kMtN - kMtM) : 0);
+  av = sbase + 16u * (uint32_t)iv;
+  am = sbase + 16u * (uint32_t)im;
+}
+
+// The twist wave: the half's state, block b -> b+1, in place (MT19937RNGEngine.h:164-175
+// on 32 seeds at once).  Round r+1's reads are issued before round r's writes: they
+// touch rows i+1 >= 64(r+1) (not written before round r+1) and rows i+397 / i-227 of
+// earlier rounds only.  U31 (plane 31 of the old row i) is the V row of lane i-1: one
+// DPP wave_shr:1, lane 0 taking the previous round's lane 63.
+__device__ __forceinline__ void bs_twist_block(uint32_t sbase, int lane) {
+  uint32_t V[32], M[32];
+  uint32_t av, am;
+  // old row 0, plane 31 (every lane the same address: a broadcast read)
+  uint32_t prev63 = lds_u32((int)(sbase + 7 * kBsChunkBytes + 12));
+  bs_round_rows(sbase, 0, lane, av, am);
+  bs_load_row(av, V);
+  bs_load_row(am, M);
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    uint32_t Vn[32], Mn[32];
+    if (r + 1 < 10) {
+      uint32_t avn, amn;
+      bs_round_rows(sbase, r + 1, lane, avn, amn);
+      bs_load_row(avn, Vn);
+      bs_load_row(amn, Mn);
+    }
+    const uint32_t u31 = (uint32_t)__builtin_amdgcn_update_dpp((int)prev63, (int)V[31], 0x138, 0xF, 0xF, false);
+    prev63 = (uint32_t)__builtin_amdgcn_readlane((int)V[31], 63);
+    bs::twist_row_inplace(V, M, u31);  // M now holds the new row i
+    if (r < 9 || 64 * r + lane < kMtN) bs_store_row(sbase + 16u * (uint32_t)(64 * r + lane), M);
+    if (r + 1 < 10) {
+#pragma unroll
+      for (int b = 0; b < 32; b++) {
+        V[b] = Vn[b];
+        M[b] = Mn[b];
+      }
+    }
+  }
+}
+
+// byte c of w times 2^S with a compile-time c (SDWA)
+template <int S>
+__device__ __forceinline__ uint32_t bs_index(uint32_t w, int c) {
+  switch (c) {
+    case 0: return bs::byte_x<0, S>(w);
+    case 1: return bs::byte_x<1, S>(w);
+    case 2: return bs::byte_x<2, S>(w);
+    default: return bs::byte_x<3, S>(w);
+  }
+}
+
+template <int MODE, bool FULL>
+__global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+  if ((uint32_t)(size_t)(lds_u32_t*)lds32 != 0u) __builtin_trap();
+  const int tid = threadIdx.x;
+  const int half = __builtin_amdgcn_readfirstlane(tid >= kBsHalfThreads ? 1 : 0);
+  const int ht = tid - half * kBsHalfThreads;
+  const int hw = __builtin_amdgcn_readfirstlane(ht >> 6);  // 0..4 pair waves, 5 twist wave
+  const int lane = tid & 63;
+  const int c = kBsChunksPerWg * (int)blockIdx.x + half;
+  const int nseeds = FULL ? kBsSeeds : a.nseeds;
+  const int64_t b0 = a.chunk_block[c], b1 = a.chunk_block[c + 1];
+  const int64_t w0 = a.chunk_block[kBsChunksPerWg * blockIdx.x];
+  const int64_t wm = a.chunk_block[kBsChunksPerWg * blockIdx.x + 1];
+  const int64_t w1 = a.chunk_block[kBsChunksPerWg * blockIdx.x + 2];
+  const int64_t nb = (wm - w0) > (w1 - wm) ? (wm - w0) : (w1 - wm);  // iterations (both halves)
+  const int64_t mynb = b1 - b0;
+  const uint32_t sbase = kBsTabBytes + (uint32_t)half * kBsStateBytes;
+
+  for (int i = tid; i < 256; i += kBsThreads) {
+    reinterpret_cast<float*>((uint8_t*)lds32)[i] = c_tab_bf16[i];
+    reinterpret_cast<float2*>((uint8_t*)lds32 + 1024)[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
+  }
+  // prologue: the jump windows of this chunk, transposed into planes
+  for (int i = ht; i < kMtN; i += kBsHalfThreads) {
+    uint32_t w[32];
+#pragma unroll
+    for (int k = 0; k < 32; k++) w[k] = k < nseeds ? a.states[((size_t)k * a.nchunks + c) * kMtN + i] : 0u;
+    bs::transpose32(w);
+    bs_store_row(sbase + 16u * (uint32_t)i, w);
+  }
+  __syncthreads();
+  // The twist wave and the pair waves run separate loops with the same barrier
+  // sequence (s_barrier is workgroup-wide whatever the program counter), so the
+  // twist's 4 x 32 row registers are never live together with the pair state.
+  if (hw == 5) {
+    if (mynb > 0) bs_twist_block(sbase, lane);  // -> block b0
+    __syncthreads();                              // state holds block b0
+    for (int64_t t = 0; t < nb; t++) {
+      __syncthreads();                            // every pair wave holds its rows of block b
+      if (t + 1 < mynb) bs_twist_block(sbase, lane);  // -> block b + 1
+      __syncthreads();
+    }
+    return;
+  }
+
+  // pair lanes (waves 0..4 of the half)
+  const bool pair_wave = true;
+  const int q = ht < kMtN / 2 ? ht : kMtN / 2 - 1;
+  const bool lane_on = pair_wave && ht < kMtN / 2;
+  const int j1 = 16 * (q >> 3) + (q & 7);
+  const bool flip = ((q >> 4) & 1) != 0;
+  const uint32_t ra_first = sbase + 16u * (uint32_t)(flip ? j1 + 8 : j1);
+  const uint32_t ra_second = sbase + 16u * (uint32_t)(flip ? j1 : j1 + 8);
+
+  float gk[kBsSeeds];
+#pragma unroll
+  for (int k = 0; k < kBsSeeds; k++) gk[k] = a.g[k];
+
+  // the lane's current segment (positions only grow)
+  int cur;
+  {
+    const int64_t s1 = (int64_t)kMtN * b0 + j1;
+    int lo = 0, hi = a.nsegs;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (a.segs[mid].start + a.segs[mid].numel <= s1) lo = mid + 1; else hi = mid;
+    }
+    cur = lo;
+  }
+  int64_t seg_start = INT64_MAX, seg_end = INT64_MAX;
+  uint64_t seg_ptr = 0;
+  float seg_lr = 0.0f, seg_wd = 0.0f;
+  bool seg_wdf = false;
+  auto load_seg = [&]() {
+    if (cur < a.nsegs) {
+      const DevSeg sg = a.segs[cur];
+      seg_start = sg.start;
+      seg_end = sg.start + sg.numel;
+      seg_ptr = sg.ptr;
+      seg_lr = sg.lr;
+      seg_wd = sg.wd;
+      seg_wdf = (sg.flags & FKS_HAS_WD) != 0;
+    } else {
+      seg_start = seg_end = INT64_MAX;
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): see fks_apply_kernel
+  };
+  if (pair_wave) load_seg();
+
+  const bool odd = (tid & 1) != 0;
+  using ST = Traits<MODE == kModeDelta ? FKS_F32 : FKS_BF16>;
+  constexpr int kEs = MODE == kModeDelta ? 4 : 2;
+  typedef typename ST::Pair Pair;
+  struct Slot { uint64_t addr; float lr, wd; uint32_t wdf; Pair raw; };
+  auto fetch = [&](int64_t b) -> Slot {
+    Slot sl;
+    const int64_t s1 = (int64_t)kMtN * b + j1;
+    while (s1 >= seg_end) { cur++; load_seg(); }
+    const bool on = lane_on && s1 >= seg_start;
+    sl.lr = seg_lr; sl.wd = seg_wd; sl.wdf = seg_wdf;
+    sl.addr = on ? seg_ptr + (uint64_t)(s1 - seg_start + (odd ? 7 : 0)) * kEs : (uint64_t)(uintptr_t)a.sink;
+    sl.raw = ST::load_pair(sl.addr);
+    return sl;
+  };
+  Slot sl;
+  if (pair_wave) {
+    sl = fetch(b0);
+    *reinterpret_cast<volatile uint32_t*>(a.sink + 1) = 0u;
+  }
+  __syncthreads();  // state holds block b0
+
+  for (int64_t t = 0; t < nb; t++) {
+    const bool act = t < mynb;  // half-uniform
+    const int64_t b = b0 + t;
+    uint32_t oa[8], ob[8];
+    if (pair_wave && act) {
+      uint32_t x[32], o1[8], o2[8];
+      bs_load_row(ra_first, x);
+      bs::temper_low8(x, o1);
+      bs_load_row(ra_second, x);
+      bs::temper_low8(x, o2);
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        oa[j] = flip ? o2[j] : o1[j];  // row j1: the radius uniforms
+        ob[j] = flip ? o1[j] : o2[j];  // row j1 + 8: the angle uniforms
+      }
+    }
+    __syncthreads();  // every pair wave holds its rows of block b (the twist wave: -> b + 1)
+    if (act) {
+      const Slot nxt = fetch(b + 1 < b1 ? b + 1 : b);
+      bs::transpose8(oa);
+      bs::transpose8(ob);
+      const uint32_t keep = odd ? ST::hi(sl.raw) : ST::lo(sl.raw);
+      const uint32_t got = swap_adjacent(odd ? ST::lo(sl.raw) : ST::hi(sl.raw));
+      f32x2_t p;
+      p.x = ST::cvt(odd ? got : keep);
+      p.y = ST::cvt(odd ? keep : got);
+#pragma unroll
+      for (int k = 0; k < kBsSeeds; k++) {
+        if (FULL || k < nseeds) {
+          const uint32_t ia = bs_index<2>(oa[k & 7], k >> 3);
+          const uint32_t ib = bs_index<3>(ob[k & 7], k >> 3);
+          const float r = lds_f32(ia);
+          const f32x2_t rr = {r, r};
+          const f32x2_t cs = lds_f32x2(1024u + ib);
+          const f32x2_t zero = {0.0f, 0.0f};
+          const f32x2_t z = rnd2<FKS_BF16>(__builtin_elementwise_fma(rr, cs, zero));
+          p = apply_pair<FKS_BF16, MODE>(p, z, gk[k], sl.lr, sl.wd, sl.wdf != 0, 0.0f);
+        }
+        // the lookups of one byte column (8 seeds) at a time: hoisting all 64 table
+        // reads ahead of the chain would spill
+        if ((k & 7) == 7) asm volatile("" ::: "memory");
+      }
+      const uint32_t b1v = ST::bits(p.x), b2v = ST::bits(p.y);
+      const uint32_t back = swap_adjacent(odd ? b1v : b2v);
+      const Pair out = odd ? ST::pack(back, b2v) : ST::pack(b1v, back);
+      ST::store_pair(sl.addr, out);
+      sl = nxt;
+    }
+    __syncthreads();  // the twist of block b + 1 is in place
+  }
+}
+
 // ------------------------------------------------------------------ irregular kernel
 // Everything the fast kernel does not take (DESIGN.md "Irregular layouts"):
 //   * runs of whole 16-blocks at any stream phase (a tensor after a ragged one, a
@@ -1206,6 +1478,39 @@ int launch_apply(int dtype, const ApplyArgs& a, void* stream) {
     case FKS_BF16 * 8 + kModePerturbUpdate: return launch_apply_t<FKS_BF16, kModePerturbUpdate>(a, stream);
     case FKS_BF16 * 8 + kModeWriteZ: return launch_apply_t<FKS_BF16, kModeWriteZ>(a, stream);
     case FKS_BF16 * 8 + kModeDelta: return launch_apply_t<FKS_BF16, kModeDelta>(a, stream);
+    default: return -FKS_ENOTSUP;
+  }
+}
+
+template <int MODE, bool FULL>
+static int launch_apply_bs_m(const ApplyBsArgs& a, void* stream) {
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fks_apply_bs_kernel<MODE, FULL>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kBsLdsBytes);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((fks_apply_bs_kernel<MODE, FULL>), dim3((unsigned)(a.nchunks / kBsChunksPerWg)),
+                     dim3(kBsThreads), kBsLdsBytes, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+template <int MODE>
+static int launch_apply_bs_t(const ApplyBsArgs& a, void* stream) {
+  return a.nseeds == kBsSeeds ? launch_apply_bs_m<MODE, true>(a, stream) : launch_apply_bs_m<MODE, false>(a, stream);
+}
+
+int launch_apply_bs(const ApplyBsArgs& a, void* stream) {
+  if (a.nseeds < 1 || a.nseeds > kBsSeeds || a.nchunks < kBsChunksPerWg || a.nchunks % kBsChunksPerWg)
+    return -FKS_EINVAL;
+  int e = ensure_tables();
+  if (e) return e;
+  switch (a.mode) {
+    case kModeUpdate: return launch_apply_bs_t<kModeUpdate>(a, stream);
+    case kModeUpdateWd: return launch_apply_bs_t<kModeUpdateWd>(a, stream);
+    case kModeUpdateNoWd: return launch_apply_bs_t<kModeUpdateNoWd>(a, stream);
+    case kModeDelta: return launch_apply_bs_t<kModeDelta>(a, stream);
     default: return -FKS_ENOTSUP;
   }
 }

@@ -136,8 +136,32 @@ struct IrrArgs {
   int32_t mode;
 };
 
+// bf16 slice kernel (fks_apply_bs_kernel): 32 seeds per pass, bit-sliced generator
+// state; one workgroup per CU holds two chunks (two 384-thread halves: 5 Box-Muller
+// pair waves + 1 twist wave each) and LDS = 3 KB of tables + 2 x 79,872 B of state.
+constexpr int kBsSeeds = 32;
+constexpr int kBsHalfThreads = 384;
+constexpr int kBsThreads = 2 * kBsHalfThreads;
+constexpr int kBsChunksPerWg = 2;
+// reconstructs of more seeds than one 19-seed pass take the slice kernel for their
+// bf16 fast segments
+constexpr int kBsMinSeeds = kMaxSeedsPerPass + 1;
+constexpr int kJumpMaxSeeds = kBsSeeds > kMaxSeedsPerPass ? kBsSeeds : kMaxSeedsPerPass;
+
+struct ApplyBsArgs {
+  const uint32_t* states;       // [nseeds][nchunks][624] generator windows at chunk starts
+  float g[kBsSeeds];            // update multiplier per seed / delta coefficient
+  const DevSeg* segs;           // bf16 fast segments, sorted by start
+  const int64_t* chunk_block;   // [nchunks + 1], nchunks = kBsChunksPerWg x workgroups
+  uint64_t* sink;               // workspace sink for idle lanes' loads/stores
+  int32_t nsegs;
+  int32_t nchunks;
+  int32_t nseeds;               // 1..32
+  int32_t mode;
+};
+
 struct JumpArgs {
-  uint64_t seeds[kMaxSeedsPerPass];
+  uint64_t seeds[kJumpMaxSeeds];
   const uint64_t* polys;        // [nchunks][312] t^(624*b-1) mod phi (unused for b == 0)
   const int64_t* chunk_block;   // [nchunks + 1]
   uint32_t* states;             // [nseeds][nchunks][624]
@@ -158,6 +182,7 @@ static_assert(sizeof(DeltaApplyDesc) == 32, "DeltaApplyDesc layout");
 // launchers (fks_device.hip); return hipError_t as int
 int launch_jump(const JumpArgs& a, int nseeds, void* stream);
 int launch_apply(int dtype, const ApplyArgs& a, void* stream);
+int launch_apply_bs(const ApplyBsArgs& a, void* stream);
 int launch_irregular(const IrrArgs& a, void* stream);
 int launch_delta_apply(const DeltaApplyDesc* d, int n, int64_t max_numel, const float* delta, void* stream);
 int device_cu_count();
