@@ -71,10 +71,13 @@ def synthetic_seeds(k):
     return seeds, scalars
 
 
+PMC_SUMMARY = "pmc_apply_r01c.json"   # the bf16 slice kernel (fks_apply_bs_kernel)
+
+
 def load_pmc_summary():
-    """Per-launch HBM traffic and VALU lane-ops per seed-element of the apply kernel,
-    from the committed rocprofv3 --pmc pass (profiles/pmc_apply_r01b.json)."""
-    p = os.path.join(ROOT, "profiles", "pmc_apply_r01b.json")
+    """Per-launch HBM traffic and VALU lane-ops per seed-element of the dominant kernel,
+    from the committed rocprofv3 --pmc pass (profiles/PMC_SUMMARY)."""
+    p = os.path.join(ROOT, "profiles", PMC_SUMMARY)
     try:
         with open(p) as f:
             return json.load(f)
@@ -182,7 +185,8 @@ def main():
     buf_bytes = total * 2
     value = buf_bytes / (dt / args.steps) / 1e9
 
-    # roofline of the dominant kernel (fks_apply_kernel), per launch, this rank
+    # roofline of the dominant kernel, per launch, this rank: the bf16 slice kernel
+    # (fks_apply_bs_kernel, 32 seeds per launch) for every reconstruct of >= 20 seeds
     rank_params = total if seed_shard else total / world
     n_apply = max(prof.n_apply, 1)
     avg_apply_s = prof.apply_ms / n_apply / 1e3
@@ -200,7 +204,7 @@ def main():
         valu = {"bound": "valu", "achieved": round(ach, 3), "peak": VALU_PEAK_TLANEOPS, "unit": "Tlane-op/s",
                 "frac": round(ach / VALU_PEAK_TLANEOPS, 4), "lane_ops_per_unit": lane_ops,
                 "unit_def": "one seed*param update (z draw + update); lane-ops = rocprofv3 SQ_INSTS_VALU x 64 per "
-                            "seed*param (profiles/pmc_apply_r01b.json); peak = non-packed VALU issue rate"}
+                            f"seed*param (profiles/{PMC_SUMMARY}); peak = non-packed VALU issue rate"}
     traffic = None if seed_shard else pmc.get("hbm_bytes_per_param_per_launch")
     if seed_shard:
         valu = None  # the committed PMC summary is the sequential kernel's
@@ -219,7 +223,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(hbm_achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(hbm_achieved / HBM_PEAK_GBS, 6),
                      "traffic": (round(traffic * rank_params) if traffic else None),
-                     "kernel": "fks_apply_kernel", "launches": prof.n_apply,
+                     "kernel": "fks_apply_bs_kernel" if len(ks) >= 20 else "fks_apply_kernel",
+                     "launches": prof.n_apply,
                      "avg_launch_ms": round(prof.apply_ms / n_apply, 3),
                      "alg_bytes_per_launch": alg_bytes},
         "roofline_valu": valu,

@@ -33,6 +33,16 @@
 #ifndef FKS_T64
 #define FKS_T64 1  // bf16 pair tempering on the 64-bit word pair (v_lshrrev_b64 / v_lshlrev_b64)
 #endif
+#ifndef FKS_BS_DIAG
+#define FKS_BS_DIAG 0  // slice kernel diagnostics (wrong results): 1 no twist, 2 no pair chain, 3 no lookups,
+                        // 4 no row reads, 5 no barriers in the block loop
+#endif
+#ifndef FKS_BS_PRIO
+#define FKS_BS_PRIO 0  // slice kernel: s_setprio of the twist wave
+#endif
+#ifndef FKS_BS_FENCE
+#define FKS_BS_FENCE 1  // slice kernel: compiler fence after every 8 seeds' table lookups
+#endif
 #ifndef FKS_RPAIR
 #define FKS_RPAIR 0  // radius table as (R,R) pairs read with ds_read_b64 (else R[256] f32, ds_read_b32)
 #endif
@@ -1027,12 +1037,14 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   // sequence (s_barrier is workgroup-wide whatever the program counter), so the
   // twist's 4 x 32 row registers are never live together with the pair state.
   if (hw == 5) {
+    // (FKS_BS_PRIO: the twist wave issuing first measured 5 % slower)
+    if (FKS_BS_PRIO) __builtin_amdgcn_s_setprio(FKS_BS_PRIO);
     if (mynb > 0) bs_twist_block(sbase, lane);  // -> block b0
     __syncthreads();                              // state holds block b0
     for (int64_t t = 0; t < nb; t++) {
-      __syncthreads();                            // every pair wave holds its rows of block b
-      if (t + 1 < mynb) bs_twist_block(sbase, lane);  // -> block b + 1
-      __syncthreads();
+      if (FKS_BS_DIAG != 5) __syncthreads();      // every pair wave holds its rows of block b
+      if (t + 1 < mynb && FKS_BS_DIAG != 1) bs_twist_block(sbase, lane);  // -> block b + 1
+      if (FKS_BS_DIAG != 5) __syncthreads();
     }
     return;
   }
@@ -1109,18 +1121,27 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
     uint32_t oa[8], ob[8];
     if (pair_wave && act) {
       uint32_t x[32], o1[8], o2[8];
+#if FKS_BS_DIAG == 4  // diagnostics: no row reads (wrong values)
+#pragma unroll
+      for (int j = 0; j < 32; j++) x[j] = (uint32_t)(b * 0x9E3779B9u) ^ (uint32_t)(j * 0x85EBCA6Bu + ht);
+      bs::temper_low8(x, o1);
+#pragma unroll
+      for (int j = 0; j < 32; j++) x[j] = (x[j] << 1) ^ (uint32_t)t;
+      bs::temper_low8(x, o2);
+#else
       bs_load_row(ra_first, x);
       bs::temper_low8(x, o1);
       bs_load_row(ra_second, x);
       bs::temper_low8(x, o2);
+#endif
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         oa[j] = flip ? o2[j] : o1[j];  // row j1: the radius uniforms
         ob[j] = flip ? o1[j] : o2[j];  // row j1 + 8: the angle uniforms
       }
     }
-    __syncthreads();  // every pair wave holds its rows of block b (the twist wave: -> b + 1)
-    if (act) {
+    if (FKS_BS_DIAG != 5) __syncthreads();  // every pair wave holds its rows of block b (twist: -> b + 1)
+    if (act && FKS_BS_DIAG != 2) {
       const Slot nxt = fetch(b + 1 < b1 ? b + 1 : b);
       bs::transpose8(oa);
       bs::transpose8(ob);
@@ -1134,16 +1155,21 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
         if (FULL || k < nseeds) {
           const uint32_t ia = bs_index<2>(oa[k & 7], k >> 3);
           const uint32_t ib = bs_index<3>(ob[k & 7], k >> 3);
+#if FKS_BS_DIAG == 3  // diagnostics: no table lookups (wrong values)
+          const f32x2_t rr = {__uint_as_float(ia | 0x3f800000u), __uint_as_float(ia | 0x3f800000u)};
+          const f32x2_t cs = {__uint_as_float(ib | 0x3f000000u), __uint_as_float(ib | 0x3e000000u)};
+#else
           const float r = lds_f32(ia);
           const f32x2_t rr = {r, r};
           const f32x2_t cs = lds_f32x2(1024u + ib);
+#endif
           const f32x2_t zero = {0.0f, 0.0f};
           const f32x2_t z = rnd2<FKS_BF16>(__builtin_elementwise_fma(rr, cs, zero));
           p = apply_pair<FKS_BF16, MODE>(p, z, gk[k], sl.lr, sl.wd, sl.wdf != 0, 0.0f);
         }
         // the lookups of one byte column (8 seeds) at a time: hoisting all 64 table
         // reads ahead of the chain would spill
-        if ((k & 7) == 7) asm volatile("" ::: "memory");
+        if (FKS_BS_FENCE && (k & 7) == 7) asm volatile("" ::: "memory");
       }
       const uint32_t b1v = ST::bits(p.x), b2v = ST::bits(p.y);
       const uint32_t back = swap_adjacent(odd ? b1v : b2v);
@@ -1151,7 +1177,7 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
       ST::store_pair(sl.addr, out);
       sl = nxt;
     }
-    __syncthreads();  // the twist of block b + 1 is in place
+    if (FKS_BS_DIAG != 5) __syncthreads();  // the twist of block b + 1 is in place
   }
 }
 

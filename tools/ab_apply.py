@@ -1,7 +1,8 @@
 """A/B timing of apply-kernel builds: python tools/ab_apply.py [lib.so ...] (no argument:
 the in-tree libfks.so).  Each build runs in its own process (FKS_LIB_OVERRIDE) on the
 same workload -- N bf16 params (default 2^28), K seeds (default 95 = 5 full passes),
-wd on -- and prints the average apply/jump launch time per 19-seed pass."""
+wd on -- and prints the average apply/jump launch time per pass (AB_SEEDS seeds per
+launch for the per-seed figure: 19, or 32 for the bf16 slice kernel)."""
 import json
 import os
 import subprocess
@@ -29,7 +30,7 @@ for _ in range(3):
     best = r if best is None else min(best, r)
 print(json.dumps({"lib": os.environ.get("FKS_LIB_OVERRIDE", "libfks.so"), "dtype": str(dt), "n": n, "k": k,
                   "apply_ms_per_launch": round(best, 3),
-                  "ps_per_seed_param": round(best * 1e9 / (n * 19), 3)}), flush=True)
+                  "ps_per_seed_param": round(best * 1e9 / (n * int(os.environ.get("AB_SEEDS", "19"))), 3)}), flush=True)
 '''
 
 

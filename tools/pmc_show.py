@@ -1,6 +1,8 @@
 """Per-dispatch averages of the PMC passes written by tools/pmc_compare.sh, for the
-FULL apply kernel (the 19-seed pass), one column per variant."""
+FULL apply kernel (the 19-seed pass; KERNEL=fks_apply_bs_kernel for the 32-seed slice
+kernel), one column per variant."""
 import csv
+import os
 import glob
 import sys
 from collections import defaultdict
@@ -10,7 +12,7 @@ def load(v):
     acc = defaultdict(list)
     for f in glob.glob(f"gpurun_out/pmc_{v}_*/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
-            if "fks_apply_kernel" in row["Kernel_Name"] and "true>" in row["Kernel_Name"]:
+            if os.environ.get("KERNEL", "fks_apply_kernel") + "<" in row["Kernel_Name"] and "true>" in row["Kernel_Name"]:
                 acc[(row["Counter_Name"], row["Dispatch_Id"])].append(float(row["Counter_Value"]))
     per = defaultdict(list)
     for (name, _), vals in acc.items():

@@ -1,4 +1,7 @@
-"""Summarise rocprofv3 output for the apply kernel into profiles/ (per-launch, per-param)."""
+"""Summarise rocprofv3 output for the dominant apply kernel into profiles/ (per-launch,
+per-param):  python tools/summarize_pmc.py TAG PARAMS SEEDS_PER_FULL_LAUNCH [KERNEL]
+(KERNEL default fks_apply_bs_kernel: the 32-seed bf16 slice kernel; fks_apply_kernel for
+the 19-seed kernel)."""
 import csv, collections, json, sys, os
 
 def per_kernel(path, name_sub):
@@ -13,11 +16,11 @@ def per_kernel(path, name_sub):
         disp[kn].add(r["Dispatch_Id"])
     return {k: {c: v / len(disp[k]) for c, v in d.items()} | {"dispatches": len(disp[k])} for k, d in agg.items()}
 
-def main(tag, params, seeds_full):
+def main(tag, params, seeds_full, kernel="fks_apply_bs_kernel"):
     base = f"gpurun_out/prof_{tag}"
-    f = per_kernel(f"{base}/pmc_fetch/bench_counter_collection.csv", "fks_apply")
-    w = per_kernel(f"{base}/pmc_write/bench_counter_collection.csv", "fks_apply")
-    sq = per_kernel(f"{base}/pmc_sq/bench_counter_collection.csv", "fks_apply")
+    f = per_kernel(f"{base}/pmc_fetch/bench_counter_collection.csv", kernel + "<")
+    w = per_kernel(f"{base}/pmc_write/bench_counter_collection.csv", kernel + "<")
+    sq = per_kernel(f"{base}/pmc_sq/bench_counter_collection.csv", kernel + "<")
     full = "apply<full>"
     fetch_kb = f[full]["FETCH_SIZE"]; write_kb = w[full]["WRITE_SIZE"]
     # gfx950: FETCH_SIZE reports 1/2 of a wide streaming read's bytes (MI355X_MICROARCH.md §HBM)
@@ -26,6 +29,7 @@ def main(tag, params, seeds_full):
     units = params * seeds_full
     out = {
         "source": f"rocprofv3 --pmc on bench.py --params {params} --k 512 (gpurun_out/prof_{tag})",
+        "kernel": kernel, "seeds_per_full_launch": seeds_full,
         "apply_full_per_launch": {"FETCH_SIZE_kB": fetch_kb, "WRITE_SIZE_kB": write_kb, **sq[full]},
         "hbm_bytes_per_launch_corrected": hbm,
         "hbm_bytes_per_param_per_launch": hbm / params,
@@ -42,6 +46,6 @@ def main(tag, params, seeds_full):
 
 if __name__ == "__main__":
     tag = sys.argv[1]; params = int(sys.argv[2]); seeds = int(sys.argv[3])
-    o = main(tag, params, seeds)
+    o = main(tag, params, seeds, *(sys.argv[4:5]))
     with open(f"profiles/pmc_apply_{tag}.json", "w") as fh:
         json.dump(o, fh, indent=1)
