@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--chunks", type=int, default=8)
     ap.add_argument("--ks", default="19,38")
     ap.add_argument("--scale", type=float, default=1.0, help="fraction of every tensor's rows (smoke runs)")
+    ap.add_argument("--progress", action="store_true", help="one stderr line per chunk (long runs)")
     args = ap.parse_args()
     from fate_llm.algo.fedkseed import codec
 
@@ -81,10 +82,14 @@ def main():
         with codec.profile() as prof:
             for c in range(args.chunks):
                 codec.directional_step(specs, ks, kv, shard=c, nshards=args.chunks)
+                if args.progress:  # chunks run back to back anyway; the sync only reports
+                    torch.cuda.synchronize()
+                    print(json.dumps({"k": k, "chunk": c, "t_s": round(time.perf_counter() - t0, 2)}),
+                          file=sys.stderr, flush=True)
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        passes = -(-k // 19)
-        samples.append({"k": k, "passes": passes, "s": round(dt, 3), "s_per_pass": round(dt / passes, 4),
+        passes = -(-len(ks) // 19)
+        samples.append({"k": len(ks), "passes": passes, "s": round(dt, 3), "s_per_pass": round(dt / passes, 4),
                         "apply_ms_per_launch": round(prof.apply_ms / max(prof.n_apply, 1), 3),
                         "launches": prof.n_apply, "jump_ms": round(prof.jump_ms, 1)})
         print(json.dumps(samples[-1]), flush=True)
