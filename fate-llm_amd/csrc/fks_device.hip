@@ -37,6 +37,9 @@
 #define FKS_BS_DIAG 0  // slice kernel diagnostics (wrong results): 1 no twist, 2 no pair chain, 3 no lookups,
                         // 4 no row reads, 5 no barriers in the block loop
 #endif
+#ifndef FKS_BS_PAIR_PRIO
+#define FKS_BS_PAIR_PRIO 0  // slice kernel: s_setprio of the pair waves
+#endif
 #ifndef FKS_BS_PRIO
 #define FKS_BS_PRIO 0  // slice kernel: s_setprio of the twist wave
 #endif
@@ -1061,6 +1064,7 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   float gk[kBsSeeds];
 #pragma unroll
   for (int k = 0; k < kBsSeeds; k++) gk[k] = a.g[k];
+  if (FKS_BS_PAIR_PRIO) __builtin_amdgcn_s_setprio(FKS_BS_PAIR_PRIO);
 
   // the lane's current segment (positions only grow)
   int cur;

@@ -92,7 +92,10 @@ constexpr int kApplyWgPerCu = FKS_APPLY_WG_PER_CU;  // resident apply workgroups
 constexpr int kMaxSeedsPerPass = (160 * 1024 / kApplyWgPerCu - 4096) / 2496 - 1;  // tables: <= 4 KB
 // calls of at most kSmallK seeds run one pass over kSmallWgPerCu workgroups per CU
 constexpr int kSmallK = 4;
-constexpr int kSmallWgPerCu = 4;  // VGPR-limited (partial-pass variants: <= 96 VGPRs, 5 waves/SIMD)
+#ifndef FKS_SMALL_WG_PER_CU
+#define FKS_SMALL_WG_PER_CU 4
+#endif
+constexpr int kSmallWgPerCu = FKS_SMALL_WG_PER_CU;  // partial-pass variants: 62-68 VGPRs
 constexpr int kJumpThreads = 1024;  // 16 waves, one chunk's jump per wave at a time
 constexpr int kJumpXLen = 19937 + 624;  // x[0..20560]: y[i + w] = x[i + w + 1], i < 19937, w < 624
 
