@@ -93,9 +93,11 @@ constexpr int kMaxSeedsPerPass = (160 * 1024 / kApplyWgPerCu - 4096) / 2496 - 1;
 // calls of at most kSmallK seeds run one pass over kSmallWgPerCu workgroups per CU
 constexpr int kSmallK = 4;
 #ifndef FKS_SMALL_WG_PER_CU
-#define FKS_SMALL_WG_PER_CU 4
+#define FKS_SMALL_WG_PER_CU 5
 #endif
-constexpr int kSmallWgPerCu = FKS_SMALL_WG_PER_CU;  // partial-pass variants: 62-68 VGPRs
+// partial-pass variants take 62-68 VGPRs (7 waves/SIMD): 5 workgroups of 5 waves fit;
+// measured per K=1 pass over the 7B layout: 4 WGs 14.5 ms, 5 WGs 12.9 ms, 6 WGs 18.6 ms
+constexpr int kSmallWgPerCu = FKS_SMALL_WG_PER_CU;
 constexpr int kJumpThreads = 1024;  // 16 waves, one chunk's jump per wave at a time
 constexpr int kJumpXLen = 19937 + 624;  // x[0..20560]: y[i + w] = x[i + w + 1], i < 19937, w < 624
 

@@ -52,7 +52,9 @@ def main():
     sweep = {}
     for k in [int(x) for x in args.ks.split(",")]:
         ks, kv = seeds[:k], [g if g != 0.0 else 1.0 for g in scalars[:k]]
-        codec.directional_step(specs, ks[:1], kv[:1])  # warm the plan caches
+        # warm the plan cache of this call's class (K <= 4: small-K plan; else the
+        # 19-seed / slice plan) so the timed call does no host-side layout work
+        codec.directional_step(specs, ks[:1] if k <= 4 else ks[:20], kv[:1] if k <= 4 else kv[:20])
         t = timed(lambda: codec.directional_step(specs, ks, kv))
         # one read + write of the buffer per pass: 32 seeds (bf16 slice kernel, k >= 20) or 19
         passes = -(-k // 32) if k >= 20 else -(-k // 19)
