@@ -37,6 +37,9 @@
 #define FKS_BS_DIAG 0  // slice kernel diagnostics (wrong results): 1 no twist, 2 no pair chain, 3 no lookups,
                         // 4 no row reads, 5 no barriers in the block loop
 #endif
+#ifndef FKS_SMALL_DBUF
+#define FKS_SMALL_DBUF 1  // passes of <= kSmallK seeds: double-buffered windows, twist overlapped
+#endif
 #ifndef FKS_BS_PAIR_PRIO
 #define FKS_BS_PAIR_PRIO 1  // slice kernel: s_setprio of the pair waves (1: 6 % faster than 0)
 #endif
@@ -533,6 +536,34 @@ __device__ __forceinline__ void twist_all(const TwistPlan& P, int nseeds) {
   twist_phase<2>(P, nseeds);
 }
 
+// Out-of-place twist of ONE window by its owner wave (double-buffered small-K kernel):
+// old words from the window at byte offset `src`, new words to the window at `dst`
+// (offsets relative to window 0 of the plan).  Phase 0 reads old words only; phases 1
+// and 2 read the new words i-227 (and word 623 the new word 0) that this wave wrote in
+// earlier phases -- a wave's LDS operations execute in order, so no barrier.  Nothing
+// else reads `dst` or writes `src` while this runs.
+template <int PH>
+__device__ __forceinline__ void twist_phase_oop(const TwistPlan& P, int src, int dst) {
+  constexpr int len = PH == 2 ? kMtN - 454 : 227;
+  constexpr int nj = (len + 63) / 64;
+  uint32_t nv[nj];
+#pragma unroll
+  for (int j = 0; j < nj; j++) {
+    const int vo = (PH == 2 && j == nj - 1 && P.lane == 41) ? P.v3last + dst : P.v[PH] + src;
+    const int mo = P.m[PH] + (PH == 0 ? src : dst);
+    nv[j] = mt_next(lds_u32(P.u[PH] + src + 256 * j), lds_u32(vo + 256 * j), lds_u32(mo + 256 * j));
+  }
+#pragma unroll
+  for (int j = 0; j < nj; j++)
+    if (j < nj - 1 || P.lane + 64 * j < len) lds_st(P.u[PH] + dst + 256 * j, nv[j]);
+}
+
+__device__ __forceinline__ void twist_oop(const TwistPlan& P, int src, int dst) {
+  twist_phase_oop<0>(P, src, dst);
+  twist_phase_oop<1>(P, src, dst);
+  twist_phase_oop<2>(P, src, dst);
+}
+
 __constant__ float c_tab_bf16[3 * 256];  // R | C | S, set once from fks::tables()
 
 // LDS: [R[256] f32 | (C,S)[256] f32x2 | windows (kMaxSeedsPerPass + 1) x 624 u32]
@@ -746,8 +777,15 @@ __device__ __forceinline__ void pair_one(const uint8_t* lds, int st_off, int k, 
   p2 = p.y;
 }
 
-template <int DT, int MODE, bool FULL>
-__global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255) / 256) void fks_apply_kernel(ApplyArgs a) {
+// DB (partial passes of <= kSmallK seeds): the windows are double-buffered -- window k
+// of buffer s at kLdsTabBytes + (s * nseeds + k) * kWinBytes, + one spare for the twist's
+// over-read -- and a sixth wave (kDbThreads) twists window 0 of block b+1 out of place
+// while the five pair waves run block b (windows 1..3 are twisted by pair waves 4..2):
+// one barrier per block instead of two, and for K=1 the twist leaves the pair waves'
+// critical path (it was a third of a K=1 pass).
+constexpr int kDbThreads = kApplyThreads + 64;
+template <int DT, int MODE, bool FULL, bool DB = false>
+__global__ __launch_bounds__(DB ? kDbThreads : kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255) / 256) void fks_apply_kernel(ApplyArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
   // the lds_* accessors address LDS by offset from 0: the dynamic block must start there
@@ -765,9 +803,10 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
       tabCS[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
     }
   }
-  for (int idx = tid; idx < nseeds * kMtN; idx += kApplyThreads) {
+  const int buf1 = DB ? nseeds * kWinBytes : 0;  // DB: the jump windows go to buffer 1
+  for (int idx = tid; idx < nseeds * kMtN; idx += (DB ? kDbThreads : kApplyThreads)) {
     const int k = idx / kMtN, i = idx - k * kMtN;
-    lds_st(kLdsTabBytes + k * kWinBytes + 4 * wperm(i), a.states[((size_t)k * a.nchunks + c) * kMtN + i]);
+    lds_st(kLdsTabBytes + buf1 + k * kWinBytes + 4 * wperm(i), a.states[((size_t)k * a.nchunks + c) * kMtN + i]);
   }
   TwistPlan plan;
   twist_plan(plan, tid, kLdsTabBytes);
@@ -777,6 +816,13 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
   for (int k = 0; k < kMaxSeedsPerPass; k++)
     gk[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(k < nseeds ? a.g[k] : 0.0f)));
   __syncthreads();
+  // DB: window tw is twisted by wave kWaves - tw (window 0 by the sixth, twist-only wave)
+  const int tw = kWaves - plan.wave;
+  const bool twister = DB && tw >= 0 && tw < nseeds;
+  if constexpr (DB) {  // block b0 into buffer 0
+    if (twister && b0 < b1) twist_oop(plan, buf1 + tw * kWinBytes, tw * kWinBytes);
+    __syncthreads();
+  }
 
   // Thread q < 312 owns Box-Muller pair q of every block: 16-block q/8, slot q%8,
   // i.e. block words j1 = 16*(q/8) + q%8 and j1 + 8 (DistributionTemplates.h:141-146).
@@ -850,9 +896,21 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
   };
   // One block: twist, prefetch block b+1 (returned), Box-Muller + update chain, store.
   auto step = [&](Slot sl, int64_t b) -> Slot {
-    __syncthreads();  // every wave is done reading block b-1's words
-    if (FKS_DIAG < 2 || FKS_DIAG == 5) twist_all(plan, nseeds);  // the raw words of stream block b
-    __syncthreads();  // every window holds block b
+    int buf = 0;  // byte offset of the buffer holding block b (DB)
+    if constexpr (DB) {
+      buf = (int)((b - b0) & 1) * nseeds * kWinBytes;
+      const int other = nseeds * kWinBytes - buf;
+      if (twister && b + 1 < b1 && (FKS_DIAG < 2 || FKS_DIAG == 5))  // block b+1, out of place
+        twist_oop(plan, buf + tw * kWinBytes, other + tw * kWinBytes);
+      if (plan.wave == kWaves) {  // the twist-only wave
+        __syncthreads();
+        return sl;
+      }
+    } else {
+      __syncthreads();  // every wave is done reading block b-1's words
+      if (FKS_DIAG < 2 || FKS_DIAG == 5) twist_all(plan, nseeds);  // the raw words of stream block b
+      __syncthreads();  // every window holds block b
+    }
     const Slot nxt = fetch(b + 1 < b1 ? b + 1 : b);  // (the last block re-reads itself, unused)
     if (FKS_DIAG != 1) {  // every lane: off lanes compute garbage into the sink
       // even lane holds (p1, partner's p1), odd lane (partner's p2, p2)
@@ -865,7 +923,7 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
         // a.g[k] straight from the kernel-argument segment (one s_load per seed): a
         // dynamically indexed gk[] would be copied to VGPRs and indexed per seed
         for (int k = 0; k < nseeds; k++)
-          pair_one<DT, MODE>(lds, st_off, k, a.g[k], sl.lr, sl.wd, sl.wdf != 0, sl.ps, p1, p2);
+          pair_one<DT, MODE>(lds, st_off + buf, k, a.g[k], sl.lr, sl.wd, sl.wdf != 0, sl.ps, p1, p2);
       }
       const uint32_t b1v = ST::bits(p1), b2v = ST::bits(p2);
       const uint32_t back = swap_adjacent(odd ? b1v : b2v);  // even gets partner's p1, odd partner's p2
@@ -875,6 +933,7 @@ __global__ __launch_bounds__(kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255
 #endif
       ST::store_pair(sl.addr, out);
     }
+    if constexpr (DB) __syncthreads();  // block b+1 is twisted; block b's buffer is free
     return nxt;
   };
   // Unrolled by two with the slots swapping roles, so the prefetched pair is consumed
@@ -1467,27 +1526,29 @@ int launch_jump(const JumpArgs& a, int nseeds, void* stream) {
   return (int)hipGetLastError();
 }
 
-template <int DT, int MODE, bool FULL>
+template <int DT, int MODE, bool FULL, bool DB = false>
 static int launch_apply_f(const ApplyArgs& a, void* stream) {
   // a partial pass allocates only its own windows (+1 spare: the twist's last-phase lanes
   // read past a window), so calls of few seeds fit more workgroups per CU
-  const size_t lds = FULL ? apply_lds_bytes() : (size_t)kLdsTabBytes + (size_t)(a.nseeds + 1) * kWinBytes;
+  const size_t lds = FULL ? apply_lds_bytes()
+                          : (size_t)kLdsTabBytes + (size_t)((DB ? 2 : 1) * a.nseeds + 1) * kWinBytes;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fks_apply_kernel<DT, MODE, FULL>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fks_apply_kernel<DT, MODE, FULL, DB>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)apply_lds_bytes());
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  hipLaunchKernelGGL((fks_apply_kernel<DT, MODE, FULL>), dim3((unsigned)a.nchunks), dim3(kApplyThreads), lds,
-                     (hipStream_t)stream, a);
+  hipLaunchKernelGGL((fks_apply_kernel<DT, MODE, FULL, DB>), dim3((unsigned)a.nchunks),
+                     dim3(DB ? kDbThreads : kApplyThreads), lds, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 
 template <int DT, int MODE>
 static int launch_apply_t(const ApplyArgs& a, void* stream) {
-  return a.nseeds == kMaxSeedsPerPass ? launch_apply_f<DT, MODE, true>(a, stream)
-                                      : launch_apply_f<DT, MODE, false>(a, stream);
+  if (a.nseeds == kMaxSeedsPerPass) return launch_apply_f<DT, MODE, true>(a, stream);
+  if (FKS_SMALL_DBUF && a.nseeds <= kSmallK) return launch_apply_f<DT, MODE, false, true>(a, stream);
+  return launch_apply_f<DT, MODE, false>(a, stream);
 }
 
 int launch_apply(int dtype, const ApplyArgs& a, void* stream) {
