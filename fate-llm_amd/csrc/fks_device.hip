@@ -35,7 +35,7 @@
 #endif
 #ifndef FKS_BS_DIAG
 #define FKS_BS_DIAG 0  // slice kernel diagnostics (wrong results): 1 no twist, 2 no pair chain, 3 no lookups,
-                        // 4 no row reads, 5 no barriers in the block loop
+                        // 5 no barriers in the block loop
 #endif
 #ifndef FKS_SMALL_DBUF
 #define FKS_SMALL_DBUF 1  // passes of <= kSmallK seeds: double-buffered windows, twist overlapped
@@ -45,6 +45,9 @@
 #endif
 #ifndef FKS_BS_PRIO
 #define FKS_BS_PRIO 0  // slice kernel: s_setprio of the twist wave
+#endif
+#ifndef FKS_BS_TAIL
+#define FKS_BS_TAIL 0  // slice kernel: seeds of a block run after barrier 2, over the next rows' reads (0: measured best; 4/8/12 put the twist on the critical path: +9 / +15 / +25 %)
 #endif
 #ifndef FKS_BS_FENCE
 #define FKS_BS_FENCE 1  // slice kernel: compiler fence after every 8 seeds' table lookups
@@ -1174,76 +1177,102 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
     sl.raw = ST::load_pair(sl.addr);
     return sl;
   };
-  Slot sl;
-  if (pair_wave) {
-    sl = fetch(b0);
-    *reinterpret_cast<volatile uint32_t*>(a.sink + 1) = 0u;
-  }
+  Slot sl = fetch(b0);
+  *reinterpret_cast<volatile uint32_t*>(a.sink + 1) = 0u;
   __syncthreads();  // state holds block b0
 
+  // rows j1 and j1 + 8 of the state -> the lane's tempered radius / angle bytes, 8 planes
+  // each (transposed to one byte per seed right before use)
+  uint32_t oa[8], ob[8];
+  auto temper_rows = [&](const uint32_t (&x1)[32], const uint32_t (&x2)[32]) {
+    uint32_t o1[8], o2[8];
+    bs::temper_low8(x1, o1);
+    bs::temper_low8(x2, o2);
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      oa[j] = flip ? o2[j] : o1[j];  // row j1: the radius uniforms
+      ob[j] = flip ? o1[j] : o2[j];  // row j1 + 8: the angle uniforms
+    }
+  };
+  // seed k's table lookups (R[a], (C,S)[b]) and its step of the update chain
+  auto lookup = [&](int k, f32x2_t& rr, f32x2_t& cs) {
+    const uint32_t ia = bs_index<2>(oa[k & 7], k >> 3);
+    const uint32_t ib = bs_index<3>(ob[k & 7], k >> 3);
+#if FKS_BS_DIAG == 3  // diagnostics: no table lookups (wrong values)
+    rr = f32x2_t{__uint_as_float(ia | 0x3f800000u), __uint_as_float(ia | 0x3f800000u)};
+    cs = f32x2_t{__uint_as_float(ib | 0x3f000000u), __uint_as_float(ib | 0x3e000000u)};
+#else
+    const float r = lds_f32(ia);
+    rr = f32x2_t{r, r};
+    cs = lds_f32x2(1024u + ib);
+#endif
+  };
+  auto chain = [&](int k, f32x2_t p, f32x2_t rr, f32x2_t cs) -> f32x2_t {
+    const f32x2_t zero = {0.0f, 0.0f};
+    const f32x2_t z = rnd2<FKS_BF16>(__builtin_elementwise_fma(rr, cs, zero));
+    return apply_pair<FKS_BF16, MODE>(p, z, gk[k], sl.lr, sl.wd, sl.wdf != 0, 0.0f);
+  };
+  if (mynb > 0) {
+    uint32_t x1[32], x2[32];
+    bs_load_row(ra_first, x1);
+    bs_load_row(ra_second, x2);
+    temper_rows(x1, x2);
+  }
+
+  // Per block: barrier 1 (every pair wave holds block b's rows; the twist wave starts
+  // block b+1) -> the first kHead seeds -> barrier 2 (block b+1 is in place) -> the last
+  // kTail seeds' lookups, then block b+1's row reads, then the tail of the chain: the
+  // row-read latency hides behind this block's last seeds instead of idling the VALU.
+  constexpr int kTail = FKS_BS_TAIL, kHead = kBsSeeds - kTail;
   for (int64_t t = 0; t < nb; t++) {
     const bool act = t < mynb;  // half-uniform
     const int64_t b = b0 + t;
-    uint32_t oa[8], ob[8];
-    if (pair_wave && act) {
-      uint32_t x[32], o1[8], o2[8];
-#if FKS_BS_DIAG == 4  // diagnostics: no row reads (wrong values)
-#pragma unroll
-      for (int j = 0; j < 32; j++) x[j] = (uint32_t)(b * 0x9E3779B9u) ^ (uint32_t)(j * 0x85EBCA6Bu + ht);
-      bs::temper_low8(x, o1);
-#pragma unroll
-      for (int j = 0; j < 32; j++) x[j] = (x[j] << 1) ^ (uint32_t)t;
-      bs::temper_low8(x, o2);
-#else
-      bs_load_row(ra_first, x);
-      bs::temper_low8(x, o1);
-      bs_load_row(ra_second, x);
-      bs::temper_low8(x, o2);
-#endif
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        oa[j] = flip ? o2[j] : o1[j];  // row j1: the radius uniforms
-        ob[j] = flip ? o1[j] : o2[j];  // row j1 + 8: the angle uniforms
-      }
-    }
-    if (FKS_BS_DIAG != 5) __syncthreads();  // every pair wave holds its rows of block b (twist: -> b + 1)
+    if (FKS_BS_DIAG != 5) __syncthreads();  // barrier 1
+    f32x2_t p = {0.0f, 0.0f};
+    Slot nxt = sl;
     if (act && FKS_BS_DIAG != 2) {
-      const Slot nxt = fetch(b + 1 < b1 ? b + 1 : b);
+      nxt = fetch(b + 1 < b1 ? b + 1 : b);
       bs::transpose8(oa);
       bs::transpose8(ob);
       const uint32_t keep = odd ? ST::hi(sl.raw) : ST::lo(sl.raw);
       const uint32_t got = swap_adjacent(odd ? ST::lo(sl.raw) : ST::hi(sl.raw));
-      f32x2_t p;
       p.x = ST::cvt(odd ? got : keep);
       p.y = ST::cvt(odd ? keep : got);
 #pragma unroll
-      for (int k = 0; k < kBsSeeds; k++) {
+      for (int k = 0; k < kHead; k++) {
         if (FULL || k < nseeds) {
-          const uint32_t ia = bs_index<2>(oa[k & 7], k >> 3);
-          const uint32_t ib = bs_index<3>(ob[k & 7], k >> 3);
-#if FKS_BS_DIAG == 3  // diagnostics: no table lookups (wrong values)
-          const f32x2_t rr = {__uint_as_float(ia | 0x3f800000u), __uint_as_float(ia | 0x3f800000u)};
-          const f32x2_t cs = {__uint_as_float(ib | 0x3f000000u), __uint_as_float(ib | 0x3e000000u)};
-#else
-          const float r = lds_f32(ia);
-          const f32x2_t rr = {r, r};
-          const f32x2_t cs = lds_f32x2(1024u + ib);
-#endif
-          const f32x2_t zero = {0.0f, 0.0f};
-          const f32x2_t z = rnd2<FKS_BF16>(__builtin_elementwise_fma(rr, cs, zero));
-          p = apply_pair<FKS_BF16, MODE>(p, z, gk[k], sl.lr, sl.wd, sl.wdf != 0, 0.0f);
+          f32x2_t rr, cs;
+          lookup(k, rr, cs);
+          p = chain(k, p, rr, cs);
         }
         // the lookups of one byte column (8 seeds) at a time: hoisting all 64 table
         // reads ahead of the chain would spill
         if (FKS_BS_FENCE && (k & 7) == 7) asm volatile("" ::: "memory");
       }
+    }
+    if (FKS_BS_DIAG != 5) __syncthreads();  // barrier 2: the twist of block b + 1 is in place
+    f32x2_t rr[kTail > 0 ? kTail : 1], cs[kTail > 0 ? kTail : 1];
+    if (act && FKS_BS_DIAG != 2) {
+#pragma unroll
+      for (int k = kHead; k < kBsSeeds; k++)
+        if (FULL || k < nseeds) lookup(k, rr[k - kHead], cs[k - kHead]);
+    }
+    asm volatile("" ::: "memory");  // the tail's lookups are issued before the row reads
+    uint32_t x1[32], x2[32];
+    bs_load_row(ra_first, x1);  // (the last block re-reads rows it does not use)
+    bs_load_row(ra_second, x2);
+    asm volatile("" ::: "memory");
+    if (act && FKS_BS_DIAG != 2) {
+#pragma unroll
+      for (int k = kHead; k < kBsSeeds; k++)
+        if (FULL || k < nseeds) p = chain(k, p, rr[k - kHead], cs[k - kHead]);
       const uint32_t b1v = ST::bits(p.x), b2v = ST::bits(p.y);
       const uint32_t back = swap_adjacent(odd ? b1v : b2v);
       const Pair out = odd ? ST::pack(back, b2v) : ST::pack(b1v, back);
       ST::store_pair(sl.addr, out);
       sl = nxt;
     }
-    if (FKS_BS_DIAG != 5) __syncthreads();  // the twist of block b + 1 is in place
+    temper_rows(x1, x2);
   }
 }
 
