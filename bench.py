@@ -71,7 +71,7 @@ def synthetic_seeds(k):
     return seeds, scalars
 
 
-PMC_SUMMARY = "pmc_apply_r01c.json"   # the bf16 slice kernel (fks_apply_bs_kernel)
+PMC_SUMMARY = "pmc_apply_r01e.json"   # the bf16 slice kernel (fks_apply_bs_kernel)
 
 
 def load_pmc_summary():
