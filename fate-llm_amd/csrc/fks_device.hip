@@ -37,6 +37,9 @@
 #define FKS_BS_DIAG 0  // slice kernel diagnostics (wrong results): 1 no twist, 2 no pair chain, 3 no lookups,
                         // 5 no barriers in the block loop
 #endif
+#ifndef FKS_DB_MIN_WAVES
+#define FKS_DB_MIN_WAVES 4  // launch-bounds waves per SIMD of the double-buffered small-K kernel (6 WGs/CU measured 19 % slower than 5 at any bound)
+#endif
 #ifndef FKS_SMALL_DBUF
 #define FKS_SMALL_DBUF 1  // passes of <= kSmallK seeds: double-buffered windows, twist overlapped
 #endif
@@ -788,7 +791,8 @@ __device__ __forceinline__ void pair_one(const uint8_t* lds, int st_off, int k, 
 // critical path (it was a third of a K=1 pass).
 constexpr int kDbThreads = kApplyThreads + 64;
 template <int DT, int MODE, bool FULL, bool DB = false>
-__global__ __launch_bounds__(DB ? kDbThreads : kApplyThreads, (kApplyWgPerCu * kApplyThreads + 255) / 256) void fks_apply_kernel(ApplyArgs a) {
+__global__ __launch_bounds__(DB ? kDbThreads : kApplyThreads,
+                             DB ? FKS_DB_MIN_WAVES : (kApplyWgPerCu * kApplyThreads + 255) / 256) void fks_apply_kernel(ApplyArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
   // the lds_* accessors address LDS by offset from 0: the dynamic block must start there
