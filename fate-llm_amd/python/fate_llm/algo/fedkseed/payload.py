@@ -1,0 +1,237 @@
+"""Compact wire format for the FedKSeed round payloads.
+
+The reference moves two Python objects per round through the FATE federation
+(pickled by the transport):
+
+* arbiter -> client, key ``"train_once"`` (fedkseed.py:57-68):
+  ``(should_exit, {"seed_candidates": LongTensor[K], "seed_probabilities": f32[K],
+  "direction_derivative_sum": dict[int, float] | None})``.  The sums dict is created
+  from ``seed_candidates`` in order (fedkseed.py:73-74) and updated in place, so it
+  carries all K keys every round, even the zero ones;
+* client -> arbiter, key ``"direction_derivative_history"`` (fedkseed.py:128,
+  trainer.py:59-66, optimizer.py:189,233): ``dict[int, list[float]]`` with all K seeds
+  as keys and one ``g.item()`` per local step appended to the sampled seed's list.
+
+This module encodes both as flat little-endian binary records and decodes them back
+to objects equal to the originals -- same key order, same float bits, the same torch
+dtypes -- so the receiving ``Trainer``/``ClientTrainer`` code runs unchanged:
+
+* seeds: u32 when every seed is in [0, 2**32) (``build_seed_candidates`` draws there),
+  else i64;
+* probabilities: the f32 tensor's bytes;
+* sums: f64 values only, when the dict's keys are exactly ``seed_candidates`` in order
+  (always, for the reference's arbiter); otherwise explicit keys as well;
+* history: CSR -- keys, u32 counts, values -- as f32 when every value round-trips
+  through f32 bit-exactly (``g.item()`` of a 0-dim f32 tensor always does), else f64.
+
+``WireContext`` wraps a federation context (the duck-typed ``ctxs_range`` / ``guest``
+/ ``hosts`` / ``arbiter`` surface fedkseed.py uses) so those two keys travel encoded
+and every other key passes through untouched: opt-in, with no change to the trainers.
+
+Host-side logic only; it touches no parameters and no device.
+"""
+import struct
+from typing import Dict, List, Mapping, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+MAGIC = b"FKSW"
+VERSION = 1
+KIND_TRAIN_ONCE = 1
+KIND_HISTORY = 2
+
+# train_once flags
+_F_EXIT = 1 << 0
+_F_SEEDS_I64 = 1 << 1
+_F_HAS_SUMS = 1 << 2
+_F_SUM_KEYS = 1 << 3      # sums carry explicit keys (order or key set differs from the seeds)
+_F_HAS_PROBS = 1 << 4
+# history flags
+_F_KEYS_I64 = 1 << 1
+_F_VALUES_F64 = 1 << 2
+
+_HEADER = struct.Struct("<4sBBHQ")  # magic, version, kind, flags, count
+_U32_MAX = 2 ** 32
+
+
+class WireFormatError(ValueError):
+    """A buffer that is not a valid FedKSeed wire record."""
+
+
+def _keys_array(keys: Sequence[int]) -> Tuple[np.ndarray, bool]:
+    a = np.asarray(keys, dtype=np.int64) if len(keys) else np.zeros(0, np.int64)
+    if a.size and (a.min() < 0 or a.max() >= _U32_MAX):
+        return a, True
+    return a.astype("<u4"), False
+
+
+def _read(buf: memoryview, off: int, dtype: str, n: int) -> Tuple[np.ndarray, int]:
+    dt = np.dtype(dtype)
+    end = off + dt.itemsize * n
+    if end > len(buf):
+        raise WireFormatError(f"truncated record: need {end} bytes, have {len(buf)}")
+    return np.frombuffer(buf[off:end], dtype=dt, count=n), end
+
+
+def _header(buf, kind: int) -> Tuple[memoryview, int, int]:
+    buf = memoryview(buf).cast("B")
+    if len(buf) < _HEADER.size:
+        raise WireFormatError("truncated header")
+    magic, version, k, flags, count = _HEADER.unpack_from(buf, 0)
+    if magic != MAGIC or version != VERSION:
+        raise WireFormatError(f"bad magic/version {magic!r}/{version}")
+    if k != kind:
+        raise WireFormatError(f"record kind {k}, expected {kind}")
+    return buf, flags, count
+
+
+def encode_train_once(message: Tuple[bool, Mapping]) -> bytes:
+    """``(should_exit, kwargs)`` of the arbiter's "train_once" put (fedkseed.py:66-68)."""
+    should_exit, kw = message
+    seeds = kw["seed_candidates"]
+    seeds_np = seeds.detach().cpu().numpy() if torch.is_tensor(seeds) else np.asarray(seeds)
+    seeds_arr, seeds_i64 = _keys_array(seeds_np.reshape(-1).tolist())
+    k = seeds_arr.size
+    probs = kw.get("seed_probabilities")
+    sums: Optional[Mapping[int, float]] = kw.get("direction_derivative_sum")
+
+    flags = (_F_EXIT if should_exit else 0) | (_F_SEEDS_I64 if seeds_i64 else 0)
+    kdt = "<i8" if seeds_i64 else "<u4"
+    parts = [seeds_arr.astype(kdt).tobytes()]
+    if probs is not None:
+        p = probs.detach().cpu() if torch.is_tensor(probs) else torch.as_tensor(probs)
+        if p.dtype != torch.float32 or p.numel() != k:
+            raise WireFormatError(f"seed_probabilities must be float32[{k}], got {p.dtype}[{p.numel()}]")
+        flags |= _F_HAS_PROBS
+        parts.append(p.contiguous().numpy().astype("<f4").tobytes())
+    if sums is not None:
+        flags |= _F_HAS_SUMS
+        keys = [int(s) for s in sums.keys()]
+        vals = np.fromiter((float(v) for v in sums.values()), dtype="<f8", count=len(keys))
+        if keys != seeds_arr.astype(np.int64).tolist():
+            flags |= _F_SUM_KEYS
+            karr, ki64 = _keys_array(keys)
+            if ki64 and not seeds_i64:
+                raise WireFormatError("sum keys outside [0, 2**32) with u32 seeds")
+            parts.append(struct.pack("<Q", len(keys)))
+            parts.append(karr.astype(kdt).tobytes())
+        parts.append(vals.tobytes())
+    return _HEADER.pack(MAGIC, VERSION, KIND_TRAIN_ONCE, flags, k) + b"".join(parts)
+
+
+def decode_train_once(buf) -> Tuple[bool, Dict]:
+    """Inverse of ``encode_train_once``: seeds as ``torch.long``, probabilities as
+    ``torch.float32``, sums as a ``dict[int, float]`` in the encoded key order."""
+    buf, flags, k = _header(buf, KIND_TRAIN_ONCE)
+    off = _HEADER.size
+    kdt = "<i8" if flags & _F_SEEDS_I64 else "<u4"
+    seeds, off = _read(buf, off, kdt, k)
+    seed_t = torch.from_numpy(seeds.astype(np.int64))
+    probs = None
+    if flags & _F_HAS_PROBS:
+        p, off = _read(buf, off, "<f4", k)
+        probs = torch.from_numpy(p.astype(np.float32))
+    sums = None
+    if flags & _F_HAS_SUMS:
+        if flags & _F_SUM_KEYS:
+            (n,), _ = _read(buf, off, "<u8", 1)
+            keys, off = _read(buf, off + 8, kdt, int(n))
+            keys = keys.astype(np.int64).tolist()
+        else:
+            keys = seed_t.tolist()
+        vals, off = _read(buf, off, "<f8", len(keys))
+        sums = dict(zip(keys, vals.tolist()))
+    if off != len(buf):
+        raise WireFormatError(f"{len(buf) - off} trailing bytes")
+    return bool(flags & _F_EXIT), {"seed_candidates": seed_t, "seed_probabilities": probs,
+                                   "direction_derivative_sum": sums}
+
+
+def encode_history(history: Mapping[int, Sequence[float]]) -> bytes:
+    """A client's ``direction_derivative_history`` (dict seed -> list of g values)."""
+    keys = [int(s) for s in history.keys()]
+    counts = np.fromiter((len(v) for v in history.values()), dtype="<u4", count=len(keys))
+    flat = np.fromiter((float(x) for v in history.values() for x in v), dtype="<f8",
+                       count=int(counts.sum()))
+    karr, ki64 = _keys_array(keys)
+    with np.errstate(over="ignore", invalid="ignore"):
+        as32 = flat.astype("<f4")
+    lossless = np.array_equal(as32.astype("<f8").view("<u8"), flat.view("<u8"))
+    flags = (_F_KEYS_I64 if ki64 else 0) | (0 if lossless else _F_VALUES_F64)
+    return (_HEADER.pack(MAGIC, VERSION, KIND_HISTORY, flags, len(keys))
+            + karr.astype("<i8" if ki64 else "<u4").tobytes() + counts.tobytes()
+            + (as32 if lossless else flat).tobytes())
+
+
+def decode_history(buf) -> Dict[int, List[float]]:
+    buf, flags, n = _header(buf, KIND_HISTORY)
+    off = _HEADER.size
+    keys, off = _read(buf, off, "<i8" if flags & _F_KEYS_I64 else "<u4", n)
+    counts, off = _read(buf, off, "<u4", n)
+    total = int(counts.astype(np.int64).sum())
+    vals, off = _read(buf, off, "<f8" if flags & _F_VALUES_F64 else "<f4", total)
+    if off != len(buf):
+        raise WireFormatError(f"{len(buf) - off} trailing bytes")
+    flat = vals.astype(np.float64).tolist()
+    out: Dict[int, List[float]] = {}
+    pos = 0
+    for key, c in zip(keys.astype(np.int64).tolist(), counts.tolist()):
+        out[key] = flat[pos:pos + c]
+        pos += c
+    return out
+
+
+_CODECS = {"train_once": (encode_train_once, decode_train_once),
+           "direction_derivative_history": (encode_history, decode_history)}
+
+
+class _WireParty:
+    """One federation party (``ctx.guest`` / a host / ``ctx.arbiter``) whose FedKSeed
+    keys are encoded on ``put`` and decoded on ``get``."""
+
+    def __init__(self, party):
+        self._party = party
+
+    def put(self, key, value):
+        codec = _CODECS.get(key)
+        return self._party.put(key, codec[0](value) if codec else value)
+
+    def get(self, key):
+        value = self._party.get(key)
+        codec = _CODECS.get(key)
+        if codec and isinstance(value, (bytes, bytearray, memoryview)):
+            return codec[1](value)
+        return value
+
+    def __getattr__(self, name):
+        return getattr(self._party, name)
+
+
+class WireContext:
+    """Wraps a federation context: ``ctxs_range`` yields wrapped sub-contexts whose
+    ``guest``, ``hosts`` and ``arbiter`` parties move the FedKSeed round payloads in
+    the compact format.  Both ends of a link must be wrapped."""
+
+    def __init__(self, ctx):
+        self._ctx = ctx
+
+    def ctxs_range(self, n):
+        for i, sub in self._ctx.ctxs_range(n):
+            yield i, WireContext(sub)
+
+    @property
+    def guest(self):
+        return _WireParty(self._ctx.guest)
+
+    @property
+    def hosts(self):
+        hosts = getattr(self._ctx, "hosts", None)
+        return [_WireParty(h) for h in hosts] if hosts else hosts
+
+    @property
+    def arbiter(self):
+        return _WireParty(self._ctx.arbiter)
+
+    def __getattr__(self, name):
+        return getattr(self._ctx, name)
