@@ -447,6 +447,7 @@ struct CachedPlan {
   std::vector<uint8_t> key;
   uint64_t hash = 0, last_use = 0;
   void* dev = nullptr;
+  int device = 0;  // the HIP device `dev` lives on
   HdrLayout H;
   HdrSizes Z;
   size_t seg_off[3] = {0, 0, 0};
@@ -546,6 +547,7 @@ CachedPlan* build_plan(const fks_tensor* t, int nt, const double* scales, uint64
   }
   put(C->H.off_runs, L.runs.data(), sizeof(DevRun) * L.runs.size());
   put(C->H.off_tiny, L.tiny.data(), sizeof(DevTiny) * L.tiny.size());
+  (void)hipGetDevice(&C->device);
   hipError_t e = hipMalloc(&C->dev, std::max<size_t>(C->H.total, 256));
   if (e != hipSuccess) {
     delete C;
@@ -559,6 +561,19 @@ CachedPlan* build_plan(const fks_tensor* t, int nt, const double* scales, uint64
     throw Error(-FKS_EHIP, std::string("plan upload: ") + hipGetErrorString(e));
   }
   return C;
+}
+
+// Free a cached header after synchronising the device that owns it (which need not be
+// the current one: the key holds the device id, so one process may cache plans of
+// several GPUs); the current device is restored.
+void free_plan(CachedPlan* C) {
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (C->device != cur) (void)hipSetDevice(C->device);
+  (void)hipDeviceSynchronize();
+  (void)hipFree(C->dev);
+  if (C->device != cur) (void)hipSetDevice(cur);
+  delete C;
 }
 
 // The cached plan for these inputs (built and uploaded on a miss).  The caller holds
@@ -582,9 +597,7 @@ CachedPlan* get_plan(const fks_tensor* t, int nt, const double* scales, uint64_t
   if (g_cache.size() >= kPlanCacheEntries) {
     auto victim = std::min_element(g_cache.begin(), g_cache.end(),
                                    [](const CachedPlan* a, const CachedPlan* b) { return a->last_use < b->last_use; });
-    (void)hipDeviceSynchronize();
-    (void)hipFree((*victim)->dev);
-    delete *victim;
+    free_plan(*victim);
     g_cache.erase(victim);
   }
   g_cache.push_back(C);
@@ -593,11 +606,7 @@ CachedPlan* get_plan(const fks_tensor* t, int nt, const double* scales, uint64_t
 
 void clear_plan_cache() {
   std::lock_guard<std::mutex> lk(g_cache_mu);
-  if (!g_cache.empty()) (void)hipDeviceSynchronize();
-  for (CachedPlan* C : g_cache) {
-    (void)hipFree(C->dev);
-    delete C;
-  }
+  for (CachedPlan* C : g_cache) free_plan(C);
   g_cache.clear();
 }
 

@@ -18,6 +18,9 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 
+#include <atomic>
+#include <mutex>
+
 #include "fks_internal.h"
 #include "fks_bitslice.h"
 
@@ -54,6 +57,12 @@
 #endif
 #ifndef FKS_BS_FENCE
 #define FKS_BS_FENCE 1  // slice kernel: compiler fence after every 8 seeds' table lookups
+#endif
+#ifndef FKS_BS_LA
+#define FKS_BS_LA 0  // slice kernel: table-lookup lookahead in seeds (0: compiler-scheduled; 4/6/8/12 measured 1.6/5.1/4.1/5.9 % slower, profiles/r02_slice_ab.log)
+#endif
+#ifndef FKS_BS_CSPACK
+#define FKS_BS_CSPACK 0  // slice kernel: (C,S) table as packed bf16 pairs (ds_read_b32) instead of f32 pairs (ds_read_b64)
 #endif
 #ifndef FKS_RPAIR
 #define FKS_RPAIR 0  // radius table as (R,R) pairs read with ds_read_b64 (else R[256] f32, ds_read_b32)
@@ -109,6 +118,8 @@ __device__ __forceinline__ float rbf_cvt(float x) {
 __device__ __forceinline__ float rbf(float x) {
 #if FKS_DIAG == 5  // diagnostics: truncation instead of RNE (wrong values)
   return __uint_as_float(__float_as_uint(x) & 0xffff0000u);
+#elif FKS_DIAG == 7  // diagnostics: no rounding at all (wrong values)
+  return x;
 #else
   return rbf_cvt(x);
 #endif
@@ -984,7 +995,11 @@ __global__ __launch_bounds__(DB ? kDbThreads : kApplyThreads,
 // mod 16 (conflict free as well).
 constexpr int kBsChunkBytes = kMtN * 16;               // 9,984
 constexpr int kBsStateBytes = 8 * kBsChunkBytes;       // 79,872
-constexpr int kBsTabBytes = 256 * 4 + 256 * 8;         // 3,072
+// (C,S): f32 pairs (8 B, ds_read_b64) or, FKS_BS_CSPACK, the two bf16 values packed in one
+// dword (4 B, ds_read_b32): a random 8-bit-indexed ds_read_b64 measured 17.4 CU-cycles per
+// wave-instruction against 6.5 for ds_read_b32 (tools/ubench/issue2.hip), for two unpack ops
+constexpr int kBsCsBytes = FKS_BS_CSPACK ? 4 : 8;
+constexpr int kBsTabBytes = 256 * 4 + 256 * kBsCsBytes;  // 2,048 (3,072)
 constexpr int kBsLdsBytes = kBsTabBytes + 2 * kBsStateBytes;  // 162,816 <= 163,840
 static_assert(kBsLdsBytes <= 163840, "slice kernel LDS");
 
@@ -1091,7 +1106,11 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
 
   for (int i = tid; i < 256; i += kBsThreads) {
     reinterpret_cast<float*>((uint8_t*)lds32)[i] = c_tab_bf16[i];
-    reinterpret_cast<float2*>((uint8_t*)lds32 + 1024)[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
+    if (FKS_BS_CSPACK)  // C in the low half, S in the high half (both exact bf16 values)
+      reinterpret_cast<uint32_t*>((uint8_t*)lds32 + 1024)[i] =
+          (__float_as_uint(c_tab_bf16[256 + i]) >> 16) | (__float_as_uint(c_tab_bf16[512 + i]) & 0xffff0000u);
+    else
+      reinterpret_cast<float2*>((uint8_t*)lds32 + 1024)[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
   }
   // prologue: the jump windows of this chunk, transposed into planes
   for (int i = ht; i < kMtN; i += kBsHalfThreads) {
@@ -1201,14 +1220,19 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   // seed k's table lookups (R[a], (C,S)[b]) and its step of the update chain
   auto lookup = [&](int k, f32x2_t& rr, f32x2_t& cs) {
     const uint32_t ia = bs_index<2>(oa[k & 7], k >> 3);
-    const uint32_t ib = bs_index<3>(ob[k & 7], k >> 3);
+    const uint32_t ib = bs_index<FKS_BS_CSPACK ? 2 : 3>(ob[k & 7], k >> 3);
 #if FKS_BS_DIAG == 3  // diagnostics: no table lookups (wrong values)
     rr = f32x2_t{__uint_as_float(ia | 0x3f800000u), __uint_as_float(ia | 0x3f800000u)};
     cs = f32x2_t{__uint_as_float(ib | 0x3f000000u), __uint_as_float(ib | 0x3e000000u)};
 #else
     const float r = lds_f32(ia);
     rr = f32x2_t{r, r};
-    cs = lds_f32x2(1024u + ib);
+    if (FKS_BS_CSPACK) {
+      const uint32_t w = lds_u32((int)(1024u + ib));
+      cs = f32x2_t{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+    } else {
+      cs = lds_f32x2(1024u + ib);
+    }
 #endif
   };
   auto chain = [&](int k, f32x2_t p, f32x2_t rr, f32x2_t cs) -> f32x2_t {
@@ -1242,16 +1266,35 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
       const uint32_t got = swap_adjacent(odd ? ST::lo(sl.raw) : ST::hi(sl.raw));
       p.x = ST::cvt(odd ? got : keep);
       p.y = ST::cvt(odd ? keep : got);
+      if (FKS_BS_LA > 0) {
+        // software-pipelined lookups: seed k + LA's table reads are issued right after
+        // seed k's chain, so each chain step waits on reads issued LA steps earlier (the
+        // compiler left on its own hoists them one seed only, and every step then waits
+        // for its own bank-conflicted reads)
+        constexpr int LA = FKS_BS_LA > 0 ? FKS_BS_LA : 1;
+        f32x2_t lrr[LA], lcs[LA];
 #pragma unroll
-      for (int k = 0; k < kHead; k++) {
-        if (FULL || k < nseeds) {
-          f32x2_t rr, cs;
-          lookup(k, rr, cs);
-          p = chain(k, p, rr, cs);
+        for (int k = 0; k < LA && k < kHead; k++)
+          if (FULL || k < nseeds) lookup(k, lrr[k], lcs[k]);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < kHead; k++) {
+          if (FULL || k < nseeds) p = chain(k, p, lrr[k % LA], lcs[k % LA]);
+          if (k + LA < kHead && (FULL || k + LA < nseeds)) lookup(k + LA, lrr[k % LA], lcs[k % LA]);
+          asm volatile("" ::: "memory");
         }
-        // the lookups of one byte column (8 seeds) at a time: hoisting all 64 table
-        // reads ahead of the chain would spill
-        if (FKS_BS_FENCE && (k & 7) == 7) asm volatile("" ::: "memory");
+      } else {
+#pragma unroll
+        for (int k = 0; k < kHead; k++) {
+          if (FULL || k < nseeds) {
+            f32x2_t rr, cs;
+            lookup(k, rr, cs);
+            p = chain(k, p, rr, cs);
+          }
+          // the lookups of one byte column (8 seeds) at a time: hoisting all 64 table
+          // reads ahead of the chain would spill
+          if (FKS_BS_FENCE && (k & 7) == 7) asm volatile("" ::: "memory");
+        }
       }
     }
     if (FKS_BS_DIAG != 5) __syncthreads();  // barrier 2: the twist of block b + 1 is in place
@@ -1522,38 +1565,64 @@ int device_cu_count() {
   return n;
 }
 
+// Once-per-DEVICE host setup: __constant__ memory and function attributes belong to
+// the device a call runs on, and one process may drive several GPUs (the plan cache
+// keys on the device id), so every such flag is a bitmask over device ids.
+class PerDevice {
+ public:
+  template <class F>
+  int run(F&& f) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -FKS_EINVAL;
+    const uint64_t bit = 1ull << dev;
+    if (done_.load(std::memory_order_acquire) & bit) return 0;
+    std::lock_guard<std::mutex> lk(mu_);
+    if (done_.load(std::memory_order_relaxed) & bit) return 0;
+    const int e = f();
+    if (e == 0) done_.fetch_or(bit, std::memory_order_release);
+    return e;
+  }
+
+ private:
+  std::mutex mu_;
+  std::atomic<uint64_t> done_{0};
+};
+
 static int ensure_tables() {
-  static int done = 0;  // per process; the constant symbols live in this code object
-  if (done) return 0;
-  const Tables& t = tables();
-  static float buf[3 * 2048];
-  for (int i = 0; i < 256; i++) {
-    buf[i] = t.r_bf16[i];
-    buf[256 + i] = t.c_bf16[i];
-    buf[512 + i] = t.s_bf16[i];
-  }
-  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_tab_bf16), buf, sizeof(float) * 768, 0, hipMemcpyHostToDevice);
-  if (e != hipSuccess) return (int)e;
-  for (int i = 0; i < 2048; i++) {
-    buf[i] = t.r_f16[i];
-    buf[2048 + i] = t.c_f16[i];
-    buf[4096 + i] = t.s_f16[i];
-  }
-  e = hipMemcpyToSymbol(HIP_SYMBOL(c_tab_f16), buf, sizeof(buf), 0, hipMemcpyHostToDevice);
-  if (e != hipSuccess) return (int)e;
-  done = 1;
-  return 0;
+  static PerDevice once;
+  return once.run([] {
+    const Tables& t = tables();
+    static float buf[3 * 2048];  // used under the PerDevice mutex only
+    for (int i = 0; i < 256; i++) {
+      buf[i] = t.r_bf16[i];
+      buf[256 + i] = t.c_bf16[i];
+      buf[512 + i] = t.s_bf16[i];
+    }
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_tab_bf16), buf, sizeof(float) * 768, 0, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return (int)e;
+    for (int i = 0; i < 2048; i++) {
+      buf[i] = t.r_f16[i];
+      buf[2048 + i] = t.c_f16[i];
+      buf[4096 + i] = t.s_f16[i];
+    }
+    e = hipMemcpyToSymbol(HIP_SYMBOL(c_tab_f16), buf, sizeof(buf), 0, hipMemcpyHostToDevice);
+    return (int)e;
+  });
+}
+
+// hipFuncAttributeMaxDynamicSharedMemorySize for kernel `fn`, once per device
+template <class K>
+static int ensure_lds_attr(PerDevice& once, K* fn, int bytes) {
+  return once.run([&] {
+    return (int)hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    bytes);
+  });
 }
 
 int launch_jump(const JumpArgs& a, int nseeds, void* stream) {
   const size_t lds = sizeof(uint32_t) * (size_t)kJumpLdsWords;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fks_jump_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-    attr = true;
-  }
+  static PerDevice attr;
+  if (int e = ensure_lds_attr(attr, &fks_jump_kernel, (int)lds)) return e;
   dim3 grid((unsigned)nseeds, (unsigned)((a.nchunks + a.chunks_per_wg - 1) / a.chunks_per_wg));
   hipLaunchKernelGGL(fks_jump_kernel, grid, dim3(kJumpThreads), lds, (hipStream_t)stream, a);
   return (int)hipGetLastError();
@@ -1565,13 +1634,8 @@ static int launch_apply_f(const ApplyArgs& a, void* stream) {
   // read past a window), so calls of few seeds fit more workgroups per CU
   const size_t lds = FULL ? apply_lds_bytes()
                           : (size_t)kLdsTabBytes + (size_t)((DB ? 2 : 1) * a.nseeds + 1) * kWinBytes;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fks_apply_kernel<DT, MODE, FULL, DB>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)apply_lds_bytes());
-    if (e != hipSuccess) return (int)e;
-    attr = true;
-  }
+  static PerDevice attr;
+  if (int e = ensure_lds_attr(attr, &fks_apply_kernel<DT, MODE, FULL, DB>, (int)apply_lds_bytes())) return e;
   hipLaunchKernelGGL((fks_apply_kernel<DT, MODE, FULL, DB>), dim3((unsigned)a.nchunks),
                      dim3(DB ? kDbThreads : kApplyThreads), lds, (hipStream_t)stream, a);
   return (int)hipGetLastError();
@@ -1611,13 +1675,8 @@ int launch_apply(int dtype, const ApplyArgs& a, void* stream) {
 
 template <int MODE, bool FULL>
 static int launch_apply_bs_m(const ApplyBsArgs& a, void* stream) {
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fks_apply_bs_kernel<MODE, FULL>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kBsLdsBytes);
-    if (e != hipSuccess) return (int)e;
-    attr = true;
-  }
+  static PerDevice attr;
+  if (int e = ensure_lds_attr(attr, &fks_apply_bs_kernel<MODE, FULL>, kBsLdsBytes)) return e;
   hipLaunchKernelGGL((fks_apply_bs_kernel<MODE, FULL>), dim3((unsigned)(a.nchunks / kBsChunksPerWg)),
                      dim3(kBsThreads), kBsLdsBytes, (hipStream_t)stream, a);
   return (int)hipGetLastError();
@@ -1645,13 +1704,8 @@ int launch_apply_bs(const ApplyBsArgs& a, void* stream) {
 template <int MODE>
 static int launch_irregular_m(const IrrArgs& a, void* stream) {
   const size_t lds = (size_t)kLdsTabBytes + sizeof(uint32_t) * (kIrrWin * (size_t)kMaxSeedsPerPass + 16);
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fks_irregular_kernel<MODE>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-    attr = true;
-  }
+  static PerDevice attr;
+  if (int e = ensure_lds_attr(attr, &fks_irregular_kernel<MODE>, (int)lds)) return e;
   hipLaunchKernelGGL((fks_irregular_kernel<MODE>), dim3((unsigned)a.nchunks), dim3(kApplyThreads), lds,
                      (hipStream_t)stream, a);
   return (int)hipGetLastError();
