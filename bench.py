@@ -5,26 +5,35 @@ One "step" = one reconstruct of the LLaMA-7B-shaped bf16 parameter buffer
 (seed, scalar) pairs -- the loop of ClientTrainer.train_once (fedkseed.py:136-141)
 -- device-resident, through the drop-in fate_llm.algo.fedkseed codec (libfks.so).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode sequential|seed-shard] [--gather]
 
-N > 1 (torch.distributed.run, one rank per GPU): the parameter stream is cut into N
-equal runs of MT19937 blocks and rank r reconstructs run r (element sharding: every
-element still sees every seed in order, so the result is bit-identical to N = 1 and
-no collective touches the data path).  Total work is fixed: "scaling": "strong".
+--gpus N > 1 without WORLD_SIZE in the environment re-launches this script under
+torch.distributed.run with N ranks (one per GPU, 127.0.0.1) as a CHILD process, before
+anything touches the GPU, and exits with its status; run under torch.distributed.run
+directly, WORLD_SIZE must equal --gpus.
 
---mode seed-shard runs the north star's C3 variant instead: rank r takes a contiguous
-1/N of the seeds, accumulates its f32 delta over the whole buffer (fks_delta_accumulate),
-one RCCL all-reduce sums the deltas over xGMI, every rank applies p = a^K p_0 - delta.
-Not the reference's rounding (DESIGN.md §7 gives its measured deviation); the default
-(--mode sequential) is the bit-exact path.
+--mode sequential (default, bit-exact): the parameter stream is cut into N equal runs of
+MT19937 blocks and rank r reconstructs run r (element sharding: every element still sees
+every seed in order, so the union is bit-identical to N = 1 and no collective touches the
+data path).  --gather adds the all-gather that leaves the whole buffer on every rank (N
+RCCL broadcasts of the shards), timed separately.  Total work is fixed: "strong" scaling.
 
-Rank 0 prints ONE JSON line: the metric, the dominant kernel's roofline (HBM, as the
-north star asks, plus the VALU roofline that actually binds), and the reference CPU
-path timed on this host in the same run (cpu_baseline).
+--mode seed-shard: the north star's C3 variant.  Rank r takes a contiguous 1/N of the
+seeds, accumulates its f32 delta over the whole buffer (fks_delta_accumulate), one RCCL
+all-reduce sums the deltas over xGMI, every rank applies p = a^K p_0 - delta.  Not the
+reference's rounding (DESIGN.md §7 gives its measured deviation).
+
+Rank 0 prints ONE JSON line: the metric, the binding roofline of the dominant kernel
+(VALU issue -- the reconstruct draws K*N normals from ~26 GB of traffic), the north
+star's HBM roofline next to it, and the reference CPU path timed on this host in the
+same run (cpu_baseline).  --selftest runs the launcher / timing / reporting logic on CPU
+ranks over gloo with a dummy step (no GPU, no codec): the CPU test of the N > 1 path.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,10 +45,17 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 LLAMA7B_PARAMS = 6_738_415_616
-HBM_PEAK_GBS = 8000.0                 # MI355X spec (MI355X_MICROARCH.md)
-# non-packed VALU issue peak: 256 CUs x 4 SIMDs x 16 lanes x 2.4 GHz (a wave64 instruction
-# occupies its SIMD for 4 cycles) = 39.3 T lane-op/s; packed f32 ops count once here
-VALU_PEAK_TLANEOPS = 256 * 4 * 16 * 2.4e9 / 1e12
+HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
+# VALU peak (MI355X_MICROARCH.md): 256 CUs x 4 SIMD-32 x 32 lanes x 2.4 GHz = 78.6 T lane-op/s
+# (a wave64 instruction every 2 cycles per SIMD).  Measured on this chip
+# (profiles/r02_ubench_issue3.log + _pmc.csv, GRBM cycles): only v_mul/v_add/v_fma/v_xor/
+# v_add_u32 co-issue two waves; every instruction the slice kernel is made of (v_cvt_pk_bf16_f32,
+# v_pk_*_f32, SDWA, v_bitop3, 64-bit shifts) issues alone at 4.43 cycles per wave-instruction
+# even at 8 waves per SIMD, so the ceiling for this mix is 1024 x 64 x 2.4e9 / 4.43.
+VALU_PEAK_TLANEOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+VALU_MIX_CYCLES = 4.43
+VALU_MIX_CEILING_TLANEOPS = 1024 * 64 * 2.4e9 / VALU_MIX_CYCLES / 1e12
+PMC_SUMMARY = "pmc_apply_r02_full.json"  # the bf16 slice kernel (fks_apply_bs_kernel), tools/summarize_pmc2.py
 
 
 def llama7b_shapes():
@@ -71,77 +87,169 @@ def synthetic_seeds(k):
     return seeds, scalars
 
 
-PMC_SUMMARY = "pmc_apply_r01e.json"   # the bf16 slice kernel (fks_apply_bs_kernel)
-
-
 def load_pmc_summary():
-    """Per-launch HBM traffic and VALU lane-ops per seed-element of the dominant kernel,
-    from the committed rocprofv3 --pmc pass (profiles/PMC_SUMMARY)."""
-    p = os.path.join(ROOT, "profiles", PMC_SUMMARY)
+    """Per-launch counters of the dominant kernel from the committed rocprofv3 --pmc
+    passes (profiles/PMC_SUMMARY, written by tools/summarize_pmc2.py)."""
     try:
-        with open(p) as f:
+        with open(os.path.join(ROOT, "profiles", PMC_SUMMARY)) as f:
             return json.load(f)
     except OSError:
         return {}
 
 
-def cpu_baseline(dtype, budget_s):
-    """The reference's CPU path (torch.manual_seed + torch.normal + the update
-    expression of zo_utils.py:49, re-typed in oracle/torch_replica.py) on a bounded
-    sample, scaled to the metric: GB/s of the 7B buffer reconstructed from K=4096."""
+# ------------------------------------------------------------------ CPU baseline
+_CPU_CHILD = r'''
+import os, sys, time, json, torch
+sys.path.insert(0, os.environ["FKS_ROOT"])
+torch.set_num_threads(1)
+from oracle import torch_replica as R
+from bench import synthetic_seeds
+n, first, step, budget = (int(os.environ[k]) for k in ("N", "FIRST", "STEP", "BUDGET"))
+s_, g_ = synthetic_seeds(4096)
+seeds = [(s, g) for s, g in zip(s_, g_) if g != 0.0]
+p = [torch.randn(n, generator=torch.Generator().manual_seed(0)).mul_(0.02).to(torch.bfloat16)]
+done, t0 = 0, time.perf_counter()
+for i in range(first, len(seeds), step):
+    if time.perf_counter() - t0 > budget:
+        break
+    s, g = seeds[i]
+    R.reconstruct(p, [s], [g], 1e-5, 0.01)
+    done += 1
+print(json.dumps({"done": done, "s": time.perf_counter() - t0}))
+'''
+
+
+def cpu_baseline(budget_s):
+    """The reference's CPU path (torch.manual_seed + torch.normal + the update expression
+    of zo_utils.py:49, re-typed in oracle/torch_replica.py) on bounded samples of the
+    same workload, scaled linearly to the 7B buffer x the 4055 non-zero seeds of K=4096:
+      * one process at torch's default thread count, at two sizes (2^22 and 2^24 bf16
+        params) to check linearity in N;
+      * the all-core variant: P = min(16, cores) single-thread processes over disjoint
+        seeds (torch.normal holds the generator mutex, so one process draws on one
+        core), the fairest CPU upper bound -- reported as `value`."""
     from oracle import torch_replica as R
     threads = torch.get_num_threads()
-    n = 1 << 24
-    p = [torch.randn(n, generator=torch.Generator().manual_seed(0)).mul_(0.02).to(dtype)]
     seeds, scalars = synthetic_seeds(4096)
-    seeds, scalars = [s for s, g in zip(seeds, scalars) if g != 0.0], [g for g in scalars if g != 0.0]
-    done, t0 = 0, time.perf_counter()
-    while done < len(seeds) and time.perf_counter() - t0 < budget_s:
-        R.reconstruct(p, seeds[done:done + 2], scalars[done:done + 2], 1e-5, 0.01)
-        done += 2
-    dt = time.perf_counter() - t0
-    ns_per = dt / (n * done) * 1e9
-    t7b = LLAMA7B_PARAMS * 4096 * 0.99 * ns_per * 1e-9
+    keep = [(s, g) for s, g in zip(seeds, scalars) if g != 0.0]
+    t7b_seeds = len(keep)
+
+    def one_process(n, budget):
+        p = [torch.randn(n, generator=torch.Generator().manual_seed(0)).mul_(0.02).to(torch.bfloat16)]
+        done, t0 = 0, time.perf_counter()
+        while done < len(keep) and time.perf_counter() - t0 < budget:
+            s, g = keep[done]
+            R.reconstruct(p, [s], [g], 1e-5, 0.01)
+            done += 1
+        dt = time.perf_counter() - t0
+        return dt / (n * done) * 1e9, done, dt
+
+    ns_small, d_small, _ = one_process(1 << 22, budget_s * 0.2)
+    ns_big, d_big, dt_big = one_process(1 << 24, budget_s * 0.3)
+    procs = max(1, min(16, os.cpu_count() or 1))
+    n_all = 1 << 22
+    env = dict(os.environ, FKS_ROOT=ROOT, N=str(n_all), STEP=str(procs), BUDGET=str(int(max(2, budget_s * 0.5))),
+               OMP_NUM_THREADS="1")
+    kids = [subprocess.Popen([sys.executable, "-c", _CPU_CHILD], env=dict(env, FIRST=str(i)), stdout=subprocess.PIPE,
+                             text=True) for i in range(procs)]
+    outs = [json.loads(k.communicate()[0].strip().splitlines()[-1]) for k in kids]
+    wall = max(o["s"] for o in outs)
+    done_all = sum(o["done"] for o in outs)
+    ns_all = wall / (n_all * done_all) * 1e9  # aggregate: ns per seed*param over all processes
+    t7b = LLAMA7B_PARAMS * t7b_seeds * ns_all * 1e-9
+    t7b_one = LLAMA7B_PARAMS * t7b_seeds * ns_big * 1e-9
     return {
-        "value": LLAMA7B_PARAMS * 2 / t7b / 1e9, "unit": "GB/s",
-        "cores": threads, "kind": "port",
-        "sample": f"torch CPU replica of zo_utils.directional_derivative_step (oracle/torch_replica.py), "
-                  f"{n} bf16 params x {done} seeds in {dt:.1f} s = {ns_per:.2f} ns per seed*param, "
-                  f"scaled linearly to 6.74e9 params x 4055 non-zero seeds ({t7b / 3600:.1f} h); "
-                  f"torch.normal holds the generator mutex (single-threaded RNG), elementwise ops on "
-                  f"{threads} threads",
+        "value": LLAMA7B_PARAMS * 2 / t7b / 1e9, "unit": "GB/s", "cores": procs, "kind": "port",
+        "sample": (f"torch CPU replica of zo_utils.directional_derivative_step (oracle/torch_replica.py), "
+                   f"{procs} single-thread processes over disjoint seeds: {done_all} seeds x {n_all} bf16 params in "
+                   f"{wall:.1f} s = {ns_all:.3f} ns per seed*param aggregate, scaled linearly to 6.74e9 params x "
+                   f"{t7b_seeds} non-zero seeds ({t7b / 3600:.1f} h)"),
+        "single_process": {"threads": threads, "ns_per_seed_param_2^22": round(ns_small, 3),
+                           "ns_per_seed_param_2^24": round(ns_big, 3), "seeds_2^22": d_small, "seeds_2^24": d_big,
+                           "seconds_2^24": round(dt_big, 1), "value_GBps": LLAMA7B_PARAMS * 2 / t7b_one / 1e9,
+                           "note": "torch.normal single-threaded under the generator mutex; elementwise ops on "
+                                   f"{threads} threads; the two sizes check linearity in N"},
+        "nproc": os.cpu_count(),
     }
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--k", type=int, default=4096)
-    ap.add_argument("--params", type=int, default=0, help="override: flat buffer of this many params (dev only)")
-    ap.add_argument("--cpu-budget", type=float, default=15.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=("sequential", "seed-shard"), default="sequential")
-    args = ap.parse_args()
+# ------------------------------------------------------------------ launcher
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+def relaunch(n: int) -> int:
+    """Run this script under torch.distributed.run with n ranks, as a child process
+    (nothing here has touched the GPU), and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.call(cmd, env=env)
+
+
+def timed_steps(step, args, world, sync):
+    for _ in range(args.warmup):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    return time.perf_counter() - t0
+
+
+def max_over_ranks(dt, world, device):
+    if world == 1:
+        return dt
+    t = torch.tensor([dt], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def selftest(args, world, rank):
+    """CPU ranks over gloo: the launcher, barrier + max-over-ranks timing and the JSON
+    line, with a dummy CPU step in place of the codec."""
+    if world > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+    x = torch.ones(1 << 16)
+
+    def step():
+        x.mul_(1.0000001)
+
+    dt = max_over_ranks(timed_steps(step, args, world, lambda: None), world, torch.device("cpu"))
+    if rank == 0:
+        print(json.dumps({"metric": "selftest", "value": args.steps / dt, "unit": "steps/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "selftest": True,
+                          "pid": os.getpid()}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+# ------------------------------------------------------------------ GPU bench
+def run(args, world, rank, local):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
+        world = dist.get_world_size()  # what RCCL reports
 
-    from fate_llm.algo.fedkseed import codec
+    from fate_llm.algo.fedkseed import codec, zo_utils
 
     dtype = torch.bfloat16
     shapes = [(args.params,)] if args.params else llama7b_shapes()
     total = sum(numel(s) for s in shapes)
     flat = torch.empty(total, dtype=dtype, device=dev)
-    gen = torch.Generator(device=dev).manual_seed(0)
-    flat.normal_(0.0, 0.02, generator=gen)
+    flat.normal_(0.0, 0.02, generator=torch.Generator(device=dev).manual_seed(0))
     views, off = [], 0
     for s in shapes:
         views.append(flat[off:off + numel(s)].view(s))
@@ -152,9 +260,9 @@ def main():
     ks, kv = [s for s, _ in keep], [g for _, g in keep]
     seed_shard = args.mode == "seed-shard"
     if seed_shard:
-        from fate_llm.algo.fedkseed import zo_utils
         groups = [{"params": views, "lr": 1e-5, "weight_decay": 0.01}]
         delta = torch.empty(total, dtype=torch.float32, device=dev)
+    shard_words = [codec.shard_range(specs, r, world) for r in range(world)] if world > 1 else [(0, total)]
 
     def step():
         if seed_shard:
@@ -162,81 +270,125 @@ def main():
         else:
             codec.directional_step(specs, ks, kv, shard=rank, nshards=world)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    sync = torch.cuda.synchronize
     with codec.profile() as prof:
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-    if world > 1:
+        dt = timed_steps(step, args, world, sync)
+    dt = max_over_ranks(dt, world, dev)
+    gather_ms = None
+    if args.gather and world > 1 and not seed_shard:
+        # every rank ends with the whole buffer: one broadcast of each element shard (the
+        # bench's buffer is one flat tensor and all its tensors are fast segments, so a
+        # shard's stream words are its element range)
+        sync()
         dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        t0 = time.perf_counter()
+        for r, (lo, hi) in enumerate(shard_words):
+            dist.broadcast(flat[lo:hi], src=r)
+        sync()
+        gather_ms = max_over_ranks(time.perf_counter() - t0, world, dev) * 1e3
+
     ms_per_step = dt / args.steps * 1e3
     buf_bytes = total * 2
     value = buf_bytes / (dt / args.steps) / 1e9
 
-    # roofline of the dominant kernel, per launch, this rank: the bf16 slice kernel
+    # ---- rooflines of the dominant kernel, this rank: the bf16 slice kernel
     # (fks_apply_bs_kernel, 32 seeds per launch) for every reconstruct of >= 20 seeds
-    rank_params = total if seed_shard else total / world
+    n_steps_prof = args.steps + args.warmup
+    rank_params = total if seed_shard else (shard_words[rank][1] - shard_words[rank][0])
     n_apply = max(prof.n_apply, 1)
     avg_apply_s = prof.apply_ms / n_apply / 1e3
     rank_seeds = len(ks) * (rank + 1) // world - len(ks) * rank // world if seed_shard else len(ks)
-    seeds_per_launch = rank_seeds * args.steps / n_apply
-    # read + write the (shard of the) buffer once: bf16 parameters, or the f32 delta
-    alg_bytes = 2 * rank_params * (4 if seed_shard else 2)
-    hbm_achieved = alg_bytes / avg_apply_s / 1e9
+    seeds_per_launch = rank_seeds * n_steps_prof / n_apply
+    units = rank_params * seeds_per_launch  # seed*param updates per launch
     pmc = load_pmc_summary()
     lane_ops = pmc.get("valu_lane_ops_per_seed_param")
-    units = rank_params * seeds_per_launch               # seed*param updates per launch
     valu = None
-    if lane_ops:
+    if lane_ops and not seed_shard:
         ach = units * lane_ops / avg_apply_s / 1e12
-        valu = {"bound": "valu", "achieved": round(ach, 3), "peak": VALU_PEAK_TLANEOPS, "unit": "Tlane-op/s",
-                "frac": round(ach / VALU_PEAK_TLANEOPS, 4), "lane_ops_per_unit": lane_ops,
-                "unit_def": "one seed*param update (z draw + update); lane-ops = rocprofv3 SQ_INSTS_VALU x 64 per "
-                            f"seed*param (profiles/{PMC_SUMMARY}); peak = non-packed VALU issue rate"}
-    traffic = None if seed_shard else pmc.get("hbm_bytes_per_param_per_launch")
-    if seed_shard:
-        valu = None  # the committed PMC summary is the sequential kernel's
+        valu = {"bound": "valu", "achieved": round(ach, 3), "peak": round(VALU_PEAK_TLANEOPS, 2), "unit": "Tlane-op/s",
+                "frac": round(ach / VALU_PEAK_TLANEOPS, 4),
+                "mix_ceiling": round(VALU_MIX_CEILING_TLANEOPS, 2),
+                "frac_of_mix_ceiling": round(ach / VALU_MIX_CEILING_TLANEOPS, 4),
+                "traffic": None,
+                "kernel": "fks_apply_bs_kernel", "launches": prof.n_apply,
+                "avg_launch_ms": round(prof.apply_ms / n_apply, 3),
+                "units_per_launch": units, "lane_ops_per_unit": round(lane_ops, 3),
+                "counters": {k: pmc.get(k) for k in ("valu_active_frac", "valu_dual_issue_frac", "wait_any_frac",
+                                                     "lds_bank_conflict_frac", "clock_ghz")},
+                "unit_def": ("one seed*param update (z draw + update chain); lane-ops = rocprofv3 SQ_INSTS_VALU x 64 "
+                             f"per seed*param (profiles/{PMC_SUMMARY}); peak = 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz "
+                             "(MI355X_MICROARCH.md); mix_ceiling = the same chip issuing this kernel's "
+                             f"single-issue instruction mix at the measured {VALU_MIX_CYCLES} cycles per "
+                             "wave-instruction (profiles/r02_ubench_issue3.log)")}
+    # the north star's roof: algorithmic HBM bytes of the WHOLE reconstruct (read + write the
+    # buffer once, SURVEY.md §8(d): 2 N elt) over the reconstruct time; the per-pass figure
+    # (each 32-seed launch streams its shard once) is reported beside it, named as such
+    elt = 4 if seed_shard else 2
+    alg_bytes_step = 2 * total * 2
+    hbm_ach = alg_bytes_step / (dt / args.steps) / 1e9
+    traffic = pmc.get("hbm_bytes_per_param_per_launch")
+    hbm = {"bound": "hbm", "achieved": round(hbm_ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(hbm_ach / HBM_PEAK_GBS, 7),
+           "traffic": (round(traffic * rank_params) if traffic and not seed_shard else None),
+           "alg_bytes_per_step": alg_bytes_step,
+           "per_pass": {"alg_bytes_per_launch": 2 * rank_params * elt,
+                        "achieved_GBps": round(2 * rank_params * elt / avg_apply_s / 1e9, 2),
+                        "note": "one launch reads + writes its shard once (32 seeds); a reconstruct is "
+                                f"{round(n_apply / n_steps_prof)} such passes"}}
     out = {
         "metric": "GB/s param buffer reconstructed from (seed,scalar) list, device-resident",
         "value": round(value, 4), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 2), "higher_is_better": True, "scaling": "strong",
-        "mode": args.mode,
-        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random-init LLaMA-7B shapes, seeded seeds/scalars)",
+        "mode": args.mode, "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (random-init LLaMA-7B shapes, seeded seeds/scalars)",
         "config": {"workload": (f"{world}xMI355X: same 7B / K={args.k}, seeds sharded {len(ks) // world}/GPU, "
                                 f"RCCL all-reduce of delta over xGMI") if seed_shard else
                    "1xMI355X: 7B-param bf16 buffer, K=4096 seeds" if world == 1 else
-                   f"{world}xMI355X: 7B-param bf16 buffer, K=4096 seeds, element-sharded",
+                   f"{world}xMI355X: 7B-param bf16 buffer, K=4096 seeds, element-sharded (bit-exact, no collective)",
                    "params": total, "k": args.k, "k_nonzero": len(ks), "tensors": len(shapes),
                    "parallelism": f"seed-shard{world}" if seed_shard else f"element-shard{world}"},
-        "roofline": {"bound": "hbm", "achieved": round(hbm_achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(hbm_achieved / HBM_PEAK_GBS, 6),
-                     "traffic": (round(traffic * rank_params) if traffic else None),
-                     "kernel": "fks_apply_bs_kernel" if len(ks) >= 20 else "fks_apply_kernel",
-                     "launches": prof.n_apply,
-                     "avg_launch_ms": round(prof.apply_ms / n_apply, 3),
-                     "alg_bytes_per_launch": alg_bytes},
-        "roofline_valu": valu,
-        "jump_kernel_ms_per_step": round(prof.jump_ms / args.steps, 2),
+        "roofline": valu if valu else hbm,
+        "roofline_hbm": hbm,
+        "jump_kernel_ms_per_step": round(prof.jump_ms / n_steps_prof, 2),
     }
+    if gather_ms is not None:
+        out["gather_ms"] = round(gather_ms, 1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(dtype, args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_budget)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--k", type=int, default=4096)
+    ap.add_argument("--params", type=int, default=0, help="override: flat buffer of this many params (dev only)")
+    ap.add_argument("--cpu-budget", type=float, default=24.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", choices=("sequential", "seed-shard"), default="sequential")
+    ap.add_argument("--gather", action="store_true", help="N > 1, sequential: all-gather the shards afterwards")
+    ap.add_argument("--selftest", action="store_true", help="CPU/gloo check of the launcher and timing logic")
+    args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return relaunch(args.gpus)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if args.selftest:
+        return selftest(args, world, rank)
+    return run(args, world, rank, local)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

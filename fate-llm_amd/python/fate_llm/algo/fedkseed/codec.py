@@ -248,6 +248,17 @@ def delta_apply(specs: Sequence[ParamSpec], delta: torch.Tensor, decays: Sequenc
         b.finish()
 
 
+def shard_range(specs: Sequence[ParamSpec], shard: int, nshards: int):
+    """Stream words [lo, hi) that element shard ``shard`` of ``nshards`` owns
+    (fks_shard_census: the clipping fks_directional_step_shard launches with).  For a
+    list of contiguous tensors laid end to end whose sizes are multiples of 16 (no tail
+    recompute words) the words are the elements of their concatenation."""
+    b = _Batch(specs)
+    rng = (ctypes.c_int64 * 2)()
+    N.check(N.load().fks_shard_census(ctypes.addressof(b.arr), b.n, int(shard), int(nshards), rng, None))
+    return int(rng[0]), int(rng[1])
+
+
 def stream_length(tensors: Sequence[torch.Tensor]) -> int:
     """32-bit MT19937 words the tensors consume per seed (their z-stream length)."""
     b = _Batch([ParamSpec(t) for t in tensors])

@@ -5,7 +5,9 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 GROUPS_=("SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU2 SQ_INSTS_VALU GRBM_GUI_ACTIVE"
          "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_CVT SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 GRBM_GUI_ACTIVE"
-         "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INSTS_VALU_INT64 SQ_BUSY_CYCLES SQ_INST_LEVEL_LDS GRBM_GUI_ACTIVE")
+         "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INSTS_VALU_INT64 SQ_BUSY_CYCLES SQ_INST_LEVEL_LDS GRBM_GUI_ACTIVE"
+         "FETCH_SIZE GRBM_GUI_ACTIVE"
+         "WRITE_SIZE GRBM_GUI_ACTIVE")
 for v in ${VARIANTS:-full}; do
   if [ "$v" != "full" ]; then export FKS_LIB_OVERRIDE=$PWD/fate-llm_amd/build/libfks_$v.so; else unset FKS_LIB_OVERRIDE; fi
   i=0
@@ -17,6 +19,7 @@ for v in ${VARIANTS:-full}; do
   done
 done
 if [ -n "$UBENCH" ]; then
+  GROUPS_=("${GROUPS_[@]:0:1}")
   i=0
   for g in "${GROUPS_[@]}"; do
     rm -rf gpurun_out/pmc2_ub_$i
@@ -26,3 +29,4 @@ if [ -n "$UBENCH" ]; then
   done
 fi
 python3 tools/pmc2_show.py ${VARIANTS:-full}
+for v in ${VARIANTS:-full}; do python3 tools/summarize_pmc2.py "${TAG:-r02}_$v" $v $((1 << 28)) 32 > /dev/null; done
