@@ -10,7 +10,11 @@ Full K=4096 is 214 passes of 19 seeds over 69e9 params (about ten minutes): the 
 times a sample of K_s seeds (whole passes) per chunk and scales linearly in the pass
 count (linearity checked on two sample sizes).  Prints one JSON line.
 
-  python tools/c4_70b.py [--chunks 8] [--ks 19,38] [--scale 1.0]
+  python tools/c4_70b.py [--chunks 8] [--ks 19,38] [--scale 1.0] [--check K]
+
+--check K (needs room for a second copy of the buffer, e.g. --scale 0.4): before timing,
+reconstruct K seeds chunked and, on a clone, in one unchunked call, and report whether
+the two agree bit for bit (tests/test_gpu_c4.py holds the oracle comparison).
 """
 import argparse
 import json
@@ -44,6 +48,7 @@ def main():
     ap.add_argument("--ks", default="19,38")
     ap.add_argument("--scale", type=float, default=1.0, help="fraction of every tensor's rows (smoke runs)")
     ap.add_argument("--progress", action="store_true", help="one stderr line per chunk (long runs)")
+    ap.add_argument("--check", type=int, default=0, help="K seeds: chunked vs unchunked, bit for bit")
     args = ap.parse_args()
     from fate_llm.algo.fedkseed import codec
 
@@ -68,6 +73,24 @@ def main():
     keep = [(s, g) for s, g in zip(seeds, scalars) if g != 0.0]
     k_full = len(keep)
     passes_full = -(-k_full // 19)
+
+    if args.check:
+        ks, kv = [s for s, _ in keep[:args.check]], [g for _, g in keep[:args.check]]
+        clone = flat.clone()
+        cviews, off = [], 0
+        for s in shapes:
+            cviews.append(clone[off:off + bench.numel(s)].view(s))
+            off += bench.numel(s)
+        for c in range(args.chunks):
+            codec.directional_step(specs, ks, kv, shard=c, nshards=args.chunks)
+        codec.directional_step([codec.ParamSpec(v, lr=1e-5, weight_decay=0.01) for v in cviews], ks, kv)
+        torch.cuda.synchronize()
+        differ = int((flat.view(torch.int32) != clone.view(torch.int32)).sum().item())
+        print(json.dumps({"check": "chunked vs unchunked", "k": len(ks), "chunks": args.chunks, "params": total,
+                          "elements_differing": differ, "bit_identical": differ == 0}), flush=True)
+        del clone, cviews
+        if differ:
+            return 2
 
     # warm the plan caches (one per chunk) with one seed
     for c in range(args.chunks):
