@@ -23,6 +23,11 @@ dtypes -- so the receiving ``Trainer``/``ClientTrainer`` code runs unchanged:
   (always, for the reference's arbiter); otherwise explicit keys as well;
 * history: CSR -- keys, u32 counts, values -- as f32 when every value round-trips
   through f32 bit-exactly (``g.item()`` of a 0-dim f32 tensor always does), else f64.
+  When both ends know the round's seed candidates and the history's keys are exactly
+  those candidates in order (always, for the reference's optimizer: optimizer.py:189),
+  only the seeds with values travel, as (candidate index, count) pairs: S local steps
+  cost 8 bytes per distinct sampled seed + 4 per value instead of 8 K + 4 S.  The
+  decoder restores the empty lists, so the object is equal to the original.
 
 ``WireContext`` wraps a federation context (the duck-typed ``ctxs_range`` / ``guest``
 / ``hosts`` / ``arbiter`` surface fedkseed.py uses) so those two keys travel encoded
@@ -50,6 +55,7 @@ _F_HAS_PROBS = 1 << 4
 # history flags
 _F_KEYS_I64 = 1 << 1
 _F_VALUES_F64 = 1 << 2
+_F_SPARSE = 1 << 3        # keys = the candidates: only (index, count) of non-empty lists
 
 _HEADER = struct.Struct("<4sBBHQ")  # magic, version, kind, flags, count
 _U32_MAX = 2 ** 32
@@ -148,26 +154,41 @@ def decode_train_once(buf) -> Tuple[bool, Dict]:
                                    "direction_derivative_sum": sums}
 
 
-def encode_history(history: Mapping[int, Sequence[float]]) -> bytes:
-    """A client's ``direction_derivative_history`` (dict seed -> list of g values)."""
+def _values_block(flat: np.ndarray) -> Tuple[int, bytes]:
+    with np.errstate(over="ignore", invalid="ignore"):
+        as32 = flat.astype("<f4")
+    lossless = np.array_equal(as32.astype("<f8").view("<u8"), flat.view("<u8"))
+    return (0 if lossless else _F_VALUES_F64), (as32 if lossless else flat).tobytes()
+
+
+def encode_history(history: Mapping[int, Sequence[float]], candidates: Optional[Sequence[int]] = None) -> bytes:
+    """A client's ``direction_derivative_history`` (dict seed -> list of g values).
+    ``candidates``: the round's seed candidates, known to both ends -- enables the
+    sparse form when the history's keys are exactly these seeds in order."""
     keys = [int(s) for s in history.keys()]
     counts = np.fromiter((len(v) for v in history.values()), dtype="<u4", count=len(keys))
     flat = np.fromiter((float(x) for v in history.values() for x in v), dtype="<f8",
                        count=int(counts.sum()))
+    vflag, vbytes = _values_block(flat)
+    if candidates is not None and keys == [int(c) for c in candidates]:
+        nz = np.nonzero(counts)[0]
+        return (_HEADER.pack(MAGIC, VERSION, KIND_HISTORY, _F_SPARSE | vflag, len(nz))
+                + nz.astype("<u4").tobytes() + counts[nz].tobytes() + vbytes)
     karr, ki64 = _keys_array(keys)
-    with np.errstate(over="ignore", invalid="ignore"):
-        as32 = flat.astype("<f4")
-    lossless = np.array_equal(as32.astype("<f8").view("<u8"), flat.view("<u8"))
-    flags = (_F_KEYS_I64 if ki64 else 0) | (0 if lossless else _F_VALUES_F64)
+    flags = (_F_KEYS_I64 if ki64 else 0) | vflag
     return (_HEADER.pack(MAGIC, VERSION, KIND_HISTORY, flags, len(keys))
-            + karr.astype("<i8" if ki64 else "<u4").tobytes() + counts.tobytes()
-            + (as32 if lossless else flat).tobytes())
+            + karr.astype("<i8" if ki64 else "<u4").tobytes() + counts.tobytes() + vbytes)
 
 
-def decode_history(buf) -> Dict[int, List[float]]:
+def decode_history(buf, candidates: Optional[Sequence[int]] = None) -> Dict[int, List[float]]:
     buf, flags, n = _header(buf, KIND_HISTORY)
     off = _HEADER.size
-    keys, off = _read(buf, off, "<i8" if flags & _F_KEYS_I64 else "<u4", n)
+    if flags & _F_SPARSE:
+        if candidates is None:
+            raise WireFormatError("sparse history record needs the round's seed candidates")
+        idx, off = _read(buf, off, "<u4", n)
+    else:
+        keys, off = _read(buf, off, "<i8" if flags & _F_KEYS_I64 else "<u4", n)
     counts, off = _read(buf, off, "<u4", n)
     total = int(counts.astype(np.int64).sum())
     vals, off = _read(buf, off, "<f8" if flags & _F_VALUES_F64 else "<f4", total)
@@ -176,32 +197,46 @@ def decode_history(buf) -> Dict[int, List[float]]:
     flat = vals.astype(np.float64).tolist()
     out: Dict[int, List[float]] = {}
     pos = 0
+    if flags & _F_SPARSE:
+        cand = [int(c) for c in candidates]
+        if n and int(idx.max()) >= len(cand):
+            raise WireFormatError("candidate index out of range")
+        got = {}
+        for i, c in zip(idx.tolist(), counts.tolist()):
+            got[i] = flat[pos:pos + c]
+            pos += c
+        return {s: got.get(i, []) for i, s in enumerate(cand)}
     for key, c in zip(keys.astype(np.int64).tolist(), counts.tolist()):
         out[key] = flat[pos:pos + c]
         pos += c
     return out
 
 
-_CODECS = {"train_once": (encode_train_once, decode_train_once),
-           "direction_derivative_history": (encode_history, decode_history)}
-
-
 class _WireParty:
     """One federation party (``ctx.guest`` / a host / ``ctx.arbiter``) whose FedKSeed
-    keys are encoded on ``put`` and decoded on ``get``."""
+    keys are encoded on ``put`` and decoded on ``get``.  The link remembers the seed
+    candidates of its last "train_once" (either direction) for the sparse history."""
 
-    def __init__(self, party):
-        self._party = party
+    def __init__(self, party, state, role):
+        self._party, self._state, self._role = party, state, role
 
     def put(self, key, value):
-        codec = _CODECS.get(key)
-        return self._party.put(key, codec[0](value) if codec else value)
+        if key == "train_once":
+            self._state[self._role] = [int(s) for s in value[1]["seed_candidates"]]
+            value = encode_train_once(value)
+        elif key == "direction_derivative_history":
+            value = encode_history(value, self._state.get(self._role))
+        return self._party.put(key, value)
 
     def get(self, key):
         value = self._party.get(key)
-        codec = _CODECS.get(key)
-        if codec and isinstance(value, (bytes, bytearray, memoryview)):
-            return codec[1](value)
+        if not isinstance(value, (bytes, bytearray, memoryview)):
+            return value
+        if key == "train_once":
+            value = decode_train_once(value)
+            self._state[self._role] = value[1]["seed_candidates"].tolist()
+        elif key == "direction_derivative_history":
+            value = decode_history(value, self._state.get(self._role))
         return value
 
     def __getattr__(self, name):
@@ -213,25 +248,26 @@ class WireContext:
     ``guest``, ``hosts`` and ``arbiter`` parties move the FedKSeed round payloads in
     the compact format.  Both ends of a link must be wrapped."""
 
-    def __init__(self, ctx):
+    def __init__(self, ctx, _state=None):
         self._ctx = ctx
+        self._state = {} if _state is None else _state  # role -> seed candidates of the link
 
     def ctxs_range(self, n):
         for i, sub in self._ctx.ctxs_range(n):
-            yield i, WireContext(sub)
+            yield i, WireContext(sub, self._state)
 
     @property
     def guest(self):
-        return _WireParty(self._ctx.guest)
+        return _WireParty(self._ctx.guest, self._state, "guest")
 
     @property
     def hosts(self):
         hosts = getattr(self._ctx, "hosts", None)
-        return [_WireParty(h) for h in hosts] if hosts else hosts
+        return [_WireParty(h, self._state, f"host{i}") for i, h in enumerate(hosts)] if hosts else hosts
 
     @property
     def arbiter(self):
-        return _WireParty(self._ctx.arbiter)
+        return _WireParty(self._ctx.arbiter, self._state, "arbiter")
 
     def __getattr__(self, name):
         return getattr(self._ctx, name)
