@@ -14,9 +14,21 @@ the directional-derivative history.
 
 The federation context is duck-typed (``ctxs_range``, ``guest``, ``hosts``,
 ``arbiter.put/get``), so ``fate.arch`` is not a dependency of this package.
+
+Round pipeline.  The reference rebuilds the model every round
+as ``copy.deepcopy(model_0).to(device)`` (fedkseed.py:132-133): a host copy of the
+whole buffer, then a pageable H2D copy.  The drop-in builds the device model directly:
+the module structure is deep-copied with every parameter and buffer already replaced by
+a device tensor, and the bytes move host -> device once, through pinned staging buffers
+on a side stream (a host-side memcpy of chunk i+1 overlaps the DMA of chunk i).  Two
+opt-in placements of ``model_0`` go further (``model_0_placement``): "pinned" pins
+model_0's host tensors once, so every round is one DMA at PCIe speed; "device" keeps a
+copy of model_0 on the device, so every round is a device-to-device copy.  All three
+give the reference's values bit for bit (copies only).
 """
 import copy
 import logging
+import threading
 from dataclasses import dataclass, field
 from typing import Dict, List, Mapping, Optional
 
@@ -90,11 +102,76 @@ class Trainer:
         pass
 
 
+_STAGE_BYTES = 64 << 20
+_STAGES = 3
+
+
+def _h2d_staged(pairs, device) -> None:
+    """dst.copy_(src) for every (device dst, host src) pair, through _STAGES pinned
+    buffers on a side stream; pinned sources go straight to the DMA.  The current stream
+    waits for the copies (the caller's next kernels see the data)."""
+    stream = torch.cuda.Stream(device)
+    bufs, ready = [], [None] * _STAGES
+    i = 0
+    with torch.cuda.stream(stream):
+        for dst, src in pairs:
+            if src.numel() == 0:
+                continue
+            if src.is_pinned():
+                dst.copy_(src, non_blocking=True)
+                continue
+            s = src.contiguous().view(-1).view(torch.uint8)
+            d = dst.view(-1).view(torch.uint8)
+            for off in range(0, s.numel(), _STAGE_BYTES):
+                n = min(_STAGE_BYTES, s.numel() - off)
+                slot = i % _STAGES
+                if len(bufs) <= slot:
+                    bufs.append(torch.empty(_STAGE_BYTES, dtype=torch.uint8, pin_memory=True))
+                if ready[slot] is not None:
+                    ready[slot].synchronize()  # the DMA that last read this buffer is done
+                bufs[slot][:n].copy_(s[off:off + n])  # host memcpy (parallel), overlaps the previous DMA
+                d[off:off + n].copy_(bufs[slot][:n], non_blocking=True)
+                ready[slot] = torch.cuda.Event()
+                ready[slot].record(stream)
+                i += 1
+    torch.cuda.current_stream(device).wait_stream(stream)
+    stream.synchronize()  # the staging buffers are released on return
+
+
+def _device_copy(module, device):
+    """copy.deepcopy(module).to(device) without the host copy: every parameter and
+    buffer is replaced by a device tensor of the same values (tied tensors stay tied)."""
+    memo, pairs = {}, []
+    tensors = list(module.named_parameters(remove_duplicate=True)) + list(module.named_buffers(remove_duplicate=True))
+    for _, t in tensors:
+        if id(t) in memo:
+            continue
+        data = torch.empty(t.shape, dtype=t.dtype, device=device)
+        pairs.append((data, t.detach()))
+        if isinstance(t, torch.nn.Parameter):
+            new = torch.nn.Parameter(data, requires_grad=t.requires_grad)
+        else:
+            new = data
+        memo[id(t)] = new
+    out = copy.deepcopy(module, memo)
+    if any(dst.device.type == "cuda" for dst, _ in pairs):
+        _h2d_staged(pairs, device)
+    else:
+        for dst, src in pairs:
+            dst.copy_(src)
+    return out
+
+
 class ClientTrainer:
-    """FedKSeed client (reference fedkseed.py:88-158)."""
+    """FedKSeed client (reference fedkseed.py:88-158).
+
+    ``model_0_placement`` (keyword, not in the reference): "host" (default; model_0
+    stays as given, each round materialises it on the device through pinned staging),
+    "pinned" (model_0's host tensors are pinned once; each round is one DMA) or
+    "device" (a device copy of model_0 is kept; each round is a device-to-device copy)."""
 
     def __init__(self, ctx, model, fedkseed_args, training_args, train_dataset, eval_dataset, data_collator,
-                 tokenizer):
+                 tokenizer, model_0_placement: str = "host"):
         self.ctx = ctx
         self.fedkseed_args = fedkseed_args
         self.training_args = training_args
@@ -104,6 +181,12 @@ class ClientTrainer:
         self.tokenizer = tokenizer
         self.weight_decay = training_args.weight_decay
         self.model_0 = model
+        if model_0_placement not in ("host", "pinned", "device"):
+            raise ValueError(f"model_0_placement must be host, pinned or device, not {model_0_placement!r}")
+        self.model_0_placement = model_0_placement
+        self._model_0_device = None
+        self._pinned = False
+        self._lock = threading.Lock()
 
     def train(self):
         for i, sub_ctx in self.ctx.ctxs_range(self.fedkseed_args.num_aggregations):
@@ -115,11 +198,28 @@ class ClientTrainer:
                                       kwargs["direction_derivative_sum"])
             sub_ctx.arbiter.put("direction_derivative_history", history)
 
+    def materialize(self, device=None):
+        """A fresh copy of model_0 on ``device`` (the training device by default): the
+        reference's copy.deepcopy(model_0).to(device) (fedkseed.py:132-133)."""
+        device = torch.device(device if device is not None else self.training_args.device)
+        if device.type != "cuda":
+            return copy.deepcopy(self.model_0).to(device)
+        with self._lock:
+            if self.model_0_placement == "device":
+                if self._model_0_device is None:
+                    self._model_0_device = _device_copy(self.model_0, device)
+                return copy.deepcopy(self._model_0_device)
+            if self.model_0_placement == "pinned" and not self._pinned:
+                for t in list(self.model_0.parameters()) + list(self.model_0.buffers()):
+                    if t.device.type == "cpu" and not t.is_pinned():
+                        t.data = t.data.pin_memory()
+                self._pinned = True
+        return _device_copy(self.model_0, device)
+
     def reconstruct(self, direction_derivative_sum: Optional[Mapping[int, float]]):
         """model_0 + every accumulated (seed, sum) step, in the dict's insertion order,
         zero sums skipped (reference :130-141), on the training device."""
-        model = copy.deepcopy(self.model_0)
-        model.to(self.training_args.device)
+        model = self.materialize()
         if direction_derivative_sum is not None:
             groups = get_optimizer_parameters_grouped_with_decay(model, self.weight_decay)
             reconstruct_(groups, list(direction_derivative_sum.keys()), list(direction_derivative_sum.values()),

@@ -5,11 +5,17 @@ round payloads through the drop-in classes:
   * the aggregator runs ``fate_llm.algo.fedkseed.fedkseed.Trainer`` unchanged: seed
     probabilities from the directional-derivative histories (probability_from_amps),
     float64 cumulative sums, one payload per client per round;
-  * each client runs ``ClientTrainer.reconstruct`` (the drop-in: deepcopy of model_0,
-    .to(device) = the H2D copy, then ONE reconstruct_ of the cumulative (seed, sum)
-    list on the MI355X codec) and S local KSeed zeroth-order steps with the drop-in
-    ``KSeedZerothOrderOptimizer`` (2 perturbations + 1 fused restore/update per step,
-    K=1 codec calls), then returns its history (scalars) to the aggregator.
+  * each client runs the drop-in ``ClientTrainer``: ``reconstruct`` (model_0 onto the
+    device -- ``--placement`` host: staged H2D through pinned buffers, pinned: model_0
+    pinned once, device: a resident copy -- then ONE reconstruct_ of the cumulative
+    (seed, sum) list on the MI355X codec) and S local KSeed zeroth-order steps, then
+    returns its history (scalars) to the aggregator.  ``--driver trainer`` runs the
+    whole ``ClientTrainer.train`` loop as the reference does, the local steps through
+    ``KSeedZOExtendedTrainer.training_step`` in the transformers training loop;
+    ``--driver optimizer`` (default) drives the drop-in ``KSeedZerothOrderOptimizer``
+    directly (2 perturbations + 1 fused restore/update per step, K=1 codec calls).
+  * ``--wire``: both ends wrap their context in payload.WireContext, so the round
+    payloads travel in the compact binary format; bytes per round are reported.
 
 The FATE transport is out of scope: payloads move as pickled objects
 over a torch.distributed gloo group (CPU), the duck-typed context the drop-in Trainer /
@@ -24,13 +30,17 @@ replays all K seeds (a late round of a long run); without it round 1 has nothing
 reconstruct, exactly as in the reference.
 
   python harness/c5_round.py [--clients N] [--rounds R] [--steps S] [--k K] [--warm]
-                             [--params P] [--resident] [--backend-device cuda|cpu]
+                             [--params P] [--placement host|pinned|device] [--driver optimizer|trainer]
+                             [--wire]
+
+Each client process sees one GPU (HIP_VISIBLE_DEVICES = client index mod GPU count), so
+several clients can share one GPU in tests.
 
 Rank 0 prints one JSON line: per-round wall time and per-phase maxima over clients.
 """
 import argparse
-import copy
 import json
+import pickle
 import os
 import socket
 import sys
@@ -51,16 +61,19 @@ class _Peer:
     """One remote party: put = send a (key, value) object, get = receive one and check
     its key (the reference's ctx.<party>.put/get, in order)."""
 
-    def __init__(self, rank):
+    def __init__(self, rank, meter):
         self.rank = rank
+        self.meter = meter  # bytes sent / received per key, as pickled by the transport
 
     def put(self, key, value):
+        self.meter[key + ".sent"] = self.meter.get(key + ".sent", 0) + len(pickle.dumps((key, value)))
         dist.send_object_list([(key, value)], dst=self.rank)
 
     def get(self, key):
         box = [None]
         dist.recv_object_list(box, src=self.rank)
         k, v = box[0]
+        self.meter[key + ".recv"] = self.meter.get(key + ".recv", 0) + len(pickle.dumps((k, v)))
         if k != key:
             raise RuntimeError(f"expected {key!r} from rank {self.rank}, got {k!r}")
         return v
@@ -71,9 +84,10 @@ class _Ctx:
     arbiter (client side)."""
 
     def __init__(self, clients, arbiter):
-        self.guest = _Peer(clients[0]) if clients else None
-        self.hosts = [_Peer(r) for r in clients[1:]]
-        self.arbiter = _Peer(arbiter) if arbiter is not None else None
+        self.meter = {}
+        self.guest = _Peer(clients[0], self.meter) if clients else None
+        self.hosts = [_Peer(r, self.meter) for r in clients[1:]]
+        self.arbiter = _Peer(arbiter, self.meter) if arbiter is not None else None
 
     def ctxs_range(self, n):
         for i in range(n):
@@ -97,7 +111,13 @@ def llama7b_shapes():
 
 class SyntheticModel(nn.Module):
     """Parameters with LLaMA-7B names and shapes (RMSNorm weights are plain parameters,
-    so, as for LlamaRMSNorm, every tensor lands in the decay group)."""
+    so, as for LlamaRMSNorm, every tensor lands in the decay group).  forward() is the
+    synthetic closure: a loss from one 4096-element slice of the first tensor (no
+    transformer forward), returned as the transformers loss output."""
+
+    def forward(self, input_ids=None, labels=None, **_):
+        probe = next(self.parameters()).view(-1)[:4096]
+        return {"loss": probe.float().square().mean() * 1e3}
 
     def __init__(self, shapes, dtype, device):
         super().__init__()
@@ -123,80 +143,108 @@ def build_model_0(shapes, seed=0):
 
 
 # ----------------------------------------------------------------------------- client
-def run_client(rank, args, arbiter_rank):
-    from fate_llm.algo.fedkseed.fedkseed import ClientTrainer, FedKSeedTrainingArguments
-    from fate_llm.algo.fedkseed.optimizer import KSeedZerothOrderOptimizer
-    from fate_llm.algo.fedkseed.pytorch_utils import get_optimizer_parameters_grouped_with_decay
+class _Steps(torch.utils.data.Dataset):
+    """S dummy batches for the transformers loop (the synthetic model ignores them)."""
 
-    ndev = torch.cuda.device_count()
-    dev = torch.device("cuda", rank % ndev)
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        return {"input_ids": torch.zeros(1, dtype=torch.long)}
+
+
+def run_client(rank, args, arbiter_rank):
+    from fate_llm.algo.fedkseed import fedkseed as F
+    from fate_llm.algo.fedkseed.optimizer import KSeedZerothOrderOptimizer
+    from fate_llm.algo.fedkseed.payload import WireContext
+    from fate_llm.algo.fedkseed.pytorch_utils import get_optimizer_parameters_grouped_with_decay
+    from fate_llm.algo.fedkseed.zo_utils import reconstruct_
+
+    dev = torch.device("cuda", 0)  # the one GPU this client process sees
     torch.cuda.set_device(dev)
     shapes = [("flat", (args.params,))] if args.params else llama7b_shapes()
     model_0 = build_model_0(shapes, seed=0)
+    fk = F.FedKSeedTrainingArguments(num_aggregations=args.rounds, k=args.k)
+    raw = _Ctx([], arbiter_rank)
+    ctx = WireContext(raw) if args.wire else raw
+    timings, received_all, histories = [], [], []
 
-    class TrainingArgs:
-        learning_rate = 1e-5
-        weight_decay = 0.0
-        device = dev
+    if args.driver == "trainer":
+        import tempfile
 
-    fk = FedKSeedTrainingArguments(num_aggregations=args.rounds, k=args.k)
-    ctx = _Ctx([], arbiter_rank)
-    trainer = ClientTrainer(ctx, model_0, fk, TrainingArgs(), None, None, None, None)
-    resident = None
-    if args.resident:  # §8(f) row 2: model_0 kept on the device across rounds
-        resident = copy.deepcopy(model_0).to(dev)
+        import transformers
+        training_args = transformers.TrainingArguments(
+            output_dir=tempfile.mkdtemp(prefix="c5_"), per_device_train_batch_size=1, max_steps=args.steps,
+            learning_rate=1e-5, weight_decay=0.0, report_to=[], save_strategy="no", logging_strategy="no",
+            max_grad_norm=0.0, dataloader_num_workers=0, disable_tqdm=True)
+    else:
+        class training_args:  # noqa: N801 -- the attributes ClientTrainer reads
+            learning_rate = 1e-5
+            weight_decay = 0.0
+            device = dev
 
-    timings = []
-    for rnd, sub in ctx.ctxs_range(args.rounds):
-        should_exit, kw = sub.arbiter.get("train_once")
-        if should_exit:
-            break
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        if resident is None:
-            # the drop-in ClientTrainer.reconstruct, phase by phase (deepcopy, H2D, codec)
-            model = copy.deepcopy(trainer.model_0)
+    class TimedClient(F.ClientTrainer):
+        """The drop-in ClientTrainer with per-phase clocks (no behavioural change)."""
+
+        def reconstruct(self, sums):
+            received_all.append(None if sums is None else {int(k): float(v) for k, v in sums.items()})
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            model = self.materialize()
+            torch.cuda.synchronize()
             t1 = time.perf_counter()
-            model.to(dev)
+            n = 0
+            if sums is not None:
+                groups = get_optimizer_parameters_grouped_with_decay(model, self.weight_decay)
+                n = reconstruct_(groups, list(sums.keys()), list(sums.values()),
+                                 lr=self.training_args.learning_rate, weight_decay=self.training_args.weight_decay)
             torch.cuda.synchronize()
-            t2 = time.perf_counter()
-        else:
-            model = copy.deepcopy(resident)  # device-to-device
+            self._t = {"t0": t0, "materialize_s": t1 - t0, "reconstruct_s": time.perf_counter() - t1,
+                       "seeds_reconstructed": n}
+            return model
+
+        def train_once(self, seed_candidates, seed_probabilities, direction_derivative_sum):
+            if args.driver == "trainer":
+                hist = super().train_once(seed_candidates, seed_probabilities, direction_derivative_sum)
+            else:
+                model = self.reconstruct(direction_derivative_sum)
+                t = time.perf_counter()
+                opt = KSeedZerothOrderOptimizer(
+                    get_optimizer_parameters_grouped_with_decay(model, self.weight_decay),
+                    seed_candidates=seed_candidates, seed_probabilities=seed_probabilities,
+                    lr=self.training_args.learning_rate, eps=fk.eps, weight_decay=self.weight_decay,
+                    grad_clip=fk.grad_clip)
+                opt.sample_random_generator.manual_seed(1000 * len(timings) + rank)  # deterministic harness
+
+                @torch.no_grad()
+                def closure():
+                    return model(input_ids=None)["loss"]
+
+                for _ in range(args.steps):
+                    opt.kseed_zeroth_order_step(closure)
+                hist = opt.directional_derivative_history
+                del model, opt
             torch.cuda.synchronize()
-            t1 = t2 = time.perf_counter()
-        sums = kw["direction_derivative_sum"]
-        n_rec = 0
-        if sums is not None:
-            from fate_llm.algo.fedkseed.zo_utils import reconstruct_
-            groups = get_optimizer_parameters_grouped_with_decay(model, TrainingArgs.weight_decay)
-            n_rec = reconstruct_(groups, list(sums.keys()), list(sums.values()), lr=TrainingArgs.learning_rate,
-                                 weight_decay=TrainingArgs.weight_decay)
-        torch.cuda.synchronize()
-        t3 = time.perf_counter()
-        opt = KSeedZerothOrderOptimizer(
-            get_optimizer_parameters_grouped_with_decay(model, TrainingArgs.weight_decay),
-            seed_candidates=kw["seed_candidates"], seed_probabilities=kw["seed_probabilities"],
-            lr=TrainingArgs.learning_rate, eps=fk.eps, weight_decay=TrainingArgs.weight_decay,
-            grad_clip=fk.grad_clip)
-        opt.sample_random_generator.manual_seed(1000 * rnd + rank)  # deterministic harness
-        probe = next(model.parameters()).view(-1)[:4096]
+            end = time.perf_counter()
+            rec = dict(self._t)
+            t0 = rec.pop("t0")
+            rec["local_steps_s"] = end - t0 - rec["materialize_s"] - rec["reconstruct_s"]
+            rec["client_round_s"] = end - t0
+            rec["round"] = len(timings)
+            timings.append(rec)
+            hist = {int(s): list(v) for s, v in hist.items()}
+            histories.append(hist)
+            return hist
 
-        @torch.no_grad()
-        def closure():
-            return probe.float().square().mean() * 1e3
-
-        for _ in range(args.steps):
-            opt.kseed_zeroth_order_step(closure)
-        torch.cuda.synchronize()
-        t4 = time.perf_counter()
-        history = {s: v for s, v in opt.directional_derivative_history.items()}
-        sub.arbiter.put("direction_derivative_history", history)
-        t5 = time.perf_counter()
-        timings.append({"round": rnd, "copy_s": t1 - t0, "h2d_s": t2 - t1, "reconstruct_s": t3 - t2,
-                        "seeds_reconstructed": n_rec, "local_steps_s": t4 - t3, "send_s": t5 - t4,
-                        "client_round_s": t5 - t0})
-        del model, opt
-    return timings
+    trainer = TimedClient(ctx, model_0, fk, training_args, _Steps(args.steps) if args.driver == "trainer" else None,
+                       None, None, None, model_0_placement=args.placement)
+    trainer.train()
+    small = args.k <= 256
+    return {"rounds": timings, "received_sums": received_all if small else None,
+            "histories": histories if small else None, "bytes": raw.meter}
 
 
 # ----------------------------------------------------------------------------- aggregator
@@ -207,7 +255,13 @@ def run_aggregator(args, clients):
     torch.manual_seed(42)
     seeds = build_seed_candidates(args.k)
     fk = FedKSeedTrainingArguments(num_aggregations=args.rounds, k=args.k)
-    ctx = _Ctx(clients, None)
+    raw = _Ctx(clients, None)
+    if args.wire:
+        from fate_llm.algo.fedkseed.payload import WireContext
+        ctx = WireContext(raw)
+    else:
+        ctx = raw
+    replies = []
 
     class WarmTrainer(Trainer):
         """Trainer.train with an optional synthetic steady state: every seed already has
@@ -234,20 +288,22 @@ def run_aggregator(args, clients):
 
     t0 = time.perf_counter()
     WarmTrainer(ctx, seeds, None, fk).train()
-    return time.perf_counter() - t0
+    return {"aggregator_s": time.perf_counter() - t0, "bytes": raw.meter, "seeds": seeds.tolist()}
 
 
-def _worker(rank, world, port, args, q):
+def _worker(rank, world, port, args, ndev, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if rank < world - 1:  # a client sees one GPU (transformers would otherwise DataParallel over all)
+        os.environ["HIP_VISIBLE_DEVICES"] = os.environ["CUDA_VISIBLE_DEVICES"] = str(rank % max(ndev, 1))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         clients = list(range(world - 1))
         arbiter = world - 1
         if rank == arbiter:
-            out = {"aggregator_s": run_aggregator(args, clients)}
+            out = run_aggregator(args, clients)
         else:
-            out = {"client": rank, "rounds": run_client(rank, args, arbiter)}
+            out = {"client": rank, **run_client(rank, args, arbiter)}
         gathered = [None] * world
         dist.all_gather_object(gathered, out)
         if rank == 0:
@@ -264,8 +320,14 @@ def main(argv=None):
     ap.add_argument("--k", type=int, default=4096)
     ap.add_argument("--params", type=int, default=0, help="flat buffer of this many params instead of 7B shapes")
     ap.add_argument("--warm", action="store_true")
-    ap.add_argument("--resident", action="store_true", help="keep model_0 on the device (no deepcopy/H2D)")
+    ap.add_argument("--resident", action="store_true", help="alias of --placement device")
+    ap.add_argument("--placement", choices=("host", "pinned", "device"), default="host",
+                    help="ClientTrainer model_0_placement")
+    ap.add_argument("--driver", choices=("optimizer", "trainer"), default="optimizer")
+    ap.add_argument("--wire", action="store_true", help="round payloads in the compact binary format")
     args = ap.parse_args(argv)
+    if args.resident:
+        args.placement = "device"
     import torch.multiprocessing as mp
 
     world = args.clients + 1
@@ -274,7 +336,8 @@ def main(argv=None):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, args, q)) for r in range(world)]
+    ndev = torch.cuda.device_count()  # counting devices does not initialise the GPU
+    procs = [ctx.Process(target=_worker, args=(r, world, port, args, ndev, q)) for r in range(world)]
     for p in procs:
         p.start()
     gathered = q.get()
@@ -284,16 +347,22 @@ def main(argv=None):
             raise SystemExit(f"a harness process exited with {p.exitcode}")
     clients = [g for g in gathered if "client" in g]
     agg = [g for g in gathered if "aggregator_s" in g][0]
+    nrounds = max(len(clients[0]["rounds"]), 1)
     rounds = []
     for r in range(len(clients[0]["rounds"])):
         per = [c["rounds"][r] for c in clients]
         rounds.append({k: (max(p[k] for p in per) if isinstance(per[0][k], float) else per[0][k]) for k in per[0]})
     nparams = args.params or sum(torch.Size(s).numel() for _, s in llama7b_shapes())
     out = {"harness": "C5 FedKSeed round", "clients": args.clients, "k": args.k, "steps": args.steps,
-           "params": nparams, "dtype": "bf16", "warm": args.warm, "resident_model_0": args.resident,
+           "params": nparams, "dtype": "bf16", "warm": args.warm, "placement": args.placement,
+           "driver": args.driver, "wire": args.wire,
            "transport": "torch.distributed gloo (stand-in for the FATE federation)",
            "rounds": [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()} for r in rounds],
-           "aggregator_total_s": round(agg["aggregator_s"], 3)}
+           "aggregator_total_s": round(agg["aggregator_s"], 3),
+           "bytes_per_round_per_client": {k: v // (nrounds * args.clients) for k, v in agg["bytes"].items()},
+           "seeds": agg["seeds"] if args.k <= 256 else None,
+           "client_received_sums": {c["client"]: c["received_sums"] for c in clients} if args.k <= 256 else None,
+           "client_histories": {c["client"]: c["histories"] for c in clients} if args.k <= 256 else None}
     print(json.dumps(out), flush=True)
     return out
 
