@@ -24,13 +24,15 @@
  * Conventions (all entry points):
  *  - plain pointers and sizes only; tensor data are DEVICE pointers, contiguous,
  *    aligned to the element size; seeds/values are HOST arrays;
- *  - the caller owns all memory; `workspace` is a device buffer of at least
- *    fks_workspace_size() bytes; nothing is allocated or freed by the library;
+ *  - the caller owns the parameters and the workspace (a device buffer of at least
+ *    fks_workspace_size() bytes); the library's only allocations are its bounded
+ *    plan cache of per-layout headers (see fks_plan_cache_clear) -- evicting an entry
+ *    synchronises the device that owns it -- and the per-device __constant__ tables;
  *  - asynchronous on `stream` (a hipStream_t; NULL = default stream), like torch ops;
  *  - return 0 on success or a negative errno-style code; fks_last_error() gives a
  *    thread-local message; no C++ exception crosses the ABI;
- *  - reentrant; the only global state is a cache of seed-independent jump-ahead
- *    polynomials (guarded by a mutex).
+ *  - reentrant; the global state (plan cache, jump-ahead polynomial cache, per-device
+ *    setup flags) is guarded by mutexes.
  */
 #ifndef FKS_H_
 #define FKS_H_
