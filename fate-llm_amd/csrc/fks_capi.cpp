@@ -352,8 +352,9 @@ HdrLayout hdr_layout(const HdrSizes& z) {
   return w;
 }
 
-// Caller's workspace: [sink 256 B | generator windows of one pass]
-constexpr size_t kWsStatesOff = 256;
+// Caller's workspace: [sink 4 KB | generator windows of one pass]; the small-K kernel's
+// lanes read a whole block's worth of sink when their block is not a fast one
+constexpr size_t kWsStatesOff = 4096;
 size_t ws_bytes_for(int chunks, int seeds_per_pass) {
   return kWsStatesOff + sizeof(uint32_t) * kMtN * (size_t)seeds_per_pass * (size_t)std::max(chunks, 1);
 }

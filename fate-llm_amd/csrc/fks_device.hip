@@ -19,6 +19,7 @@
 #include <hip/hip_bf16.h>
 
 #include <atomic>
+#include <type_traits>
 #include <mutex>
 
 #include "fks_internal.h"
@@ -43,6 +44,21 @@
 #ifndef FKS_DB_MIN_WAVES
 #define FKS_DB_MIN_WAVES 4  // launch-bounds waves per SIMD of the double-buffered small-K kernel (6 WGs/CU measured 19 % slower than 5 at any bound)
 #endif
+#ifndef FKS_SM2_PF
+#define FKS_SM2_PF 1  // small-K kernel parameter prefetch distance in blocks (1 or 2)
+#endif
+#ifndef FKS_SM2_TWREG
+#define FKS_SM2_TWREG 1  // small-K twist wave: phases chained in registers (twist_oop_reg)
+#endif
+#ifndef FKS_SM2_ROT
+#define FKS_SM2_ROT 0  // small-K kernel: rotate the twist role across the workgroups' waves
+#endif
+#ifndef FKS_SM2_TAB
+#define FKS_SM2_TAB 0  // small-K kernel bf16 table layout: 0 R|(C,S) f32x2, 1 R|C|S f32, 2 R|(C,S) packed bf16
+#endif
+#ifndef FKS_SM2_MIN_WAVES
+#define FKS_SM2_MIN_WAVES 8  // launch-bounds waves per SIMD of fks_small2_kernel (8 workgroups of 4 waves per CU: <= 64 VGPRs)
+#endif
 #ifndef FKS_SMALL_DBUF
 #define FKS_SMALL_DBUF 1  // passes of <= kSmallK seeds: double-buffered windows, twist overlapped
 #endif
@@ -64,8 +80,11 @@
 #ifndef FKS_BS_CSPACK
 #define FKS_BS_CSPACK 0  // slice kernel: (C,S) table as packed bf16 pairs (ds_read_b32) instead of f32 pairs (ds_read_b64)
 #endif
+#ifndef FKS_TEMPER_FOLD
+#define FKS_TEMPER_FOLD 1  // bf16 pair tempering with the third step folded into the index (temper_pair_u8x8)
+#endif
 #ifndef FKS_RPAIR
-#define FKS_RPAIR 0  // radius table as (R,R) pairs read with ds_read_b64 (else R[256] f32, ds_read_b32)
+#define FKS_RPAIR 0  // radius table as (R,R) pairs read with ds_read_b64 (1) or one dword of the pair at the x8 index (2); 0: R[256] f32, ds_read_b32
 #endif
 
 namespace fks {
@@ -581,6 +600,47 @@ __device__ __forceinline__ void twist_oop(const TwistPlan& P, int src, int dst) 
   twist_phase_oop<2>(P, src, dst);
 }
 
+// The same out-of-place twist with the phases chained in REGISTERS: lane l's word
+// i = lo + l + 64 j of phase 1 (2) takes as m the new word i - 227, which is this lane's
+// own word (l, j) of phase 0 (1); only word 623's partner, the new word 0, crosses lanes
+// (lane 0's first word, broadcast with v_readlane).  So every LDS read of the window is
+// issued up front, against the old words only, and there is one LDS round trip per
+// window instead of three dependent ones.
+__device__ __forceinline__ void twist_oop_reg(const TwistPlan& P, int src, int dst) {
+  uint32_t u0[4], v0[4], m0[4], u1[4], v1[4], u2[3], v2[3];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    u0[j] = lds_u32(P.u[0] + src + 256 * j);
+    v0[j] = lds_u32(P.v[0] + src + 256 * j);
+    m0[j] = lds_u32(P.m[0] + src + 256 * j);
+    u1[j] = lds_u32(P.u[1] + src + 256 * j);
+    v1[j] = lds_u32(P.v[1] + src + 256 * j);
+  }
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    u2[j] = lds_u32(P.u[2] + src + 256 * j);
+    v2[j] = lds_u32(P.v[2] + src + 256 * j);  // lane 41, j = 2 (i = 623): replaced below
+  }
+  uint32_t n0[4], n1[4], n2[3];
+#pragma unroll
+  for (int j = 0; j < 4; j++) n0[j] = mt_next(u0[j], v0[j], m0[j]);
+#pragma unroll
+  for (int j = 0; j < 4; j++) n1[j] = mt_next(u1[j], v1[j], n0[j]);
+  const uint32_t x0 = __builtin_amdgcn_readlane(n0[0], 0);
+#pragma unroll
+  for (int j = 0; j < 3; j++) n2[j] = mt_next(u2[j], (j == 2 && P.lane == 41) ? x0 : v2[j], n1[j]);
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    if (j < 3 || P.lane + 192 < 227) {
+      lds_st(P.u[0] + dst + 256 * j, n0[j]);
+      lds_st(P.u[1] + dst + 256 * j, n1[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 3; j++)
+    if (j < 2 || P.lane + 128 < kMtN - 454) lds_st(P.u[2] + dst + 256 * j, n2[j]);
+}
+
 __constant__ float c_tab_bf16[3 * 256];  // R | C | S, set once from fks::tables()
 
 // LDS: [R[256] f32 | (C,S)[256] f32x2 | windows (kMaxSeedsPerPass + 1) x 624 u32]
@@ -620,6 +680,20 @@ __device__ __forceinline__ u32x2_t temper_pair_u8x8(u32x2_t y) {
   t = shl64<7>(y);
   y.x = __builtin_amdgcn_bitop3_b32(y.x, t.x, 0x9d2c5680u, kXorAnd);
   y.y = __builtin_amdgcn_bitop3_b32(y.y, t.y, 0x9d2c5680u, kXorAnd);
+#if FKS_TEMPER_FOLD
+  // the third step y ^= (y << 15) & 0xefc60000 changes bits 17..31 only; of those the
+  // index reads bits 18..25, where it adds y bits 3..10 under 0xF1 (= 0xefc60000 >> 18):
+  // idx8 = ((y << 3) ^ (y >> 15) ^ (y & 0x788)) & 0x7F8 on the second step's y -- 6 ops
+  // for the pair instead of 7 (checked against the four-step tempering in
+  // tests/test_temper_fold.py)
+  const u32x2_t t1 = shl64<3>(y), t2 = shr64<15>(y);
+  u32x2_t o;
+  o.x = __builtin_amdgcn_bitop3_b32(t1.x, t2.x, 0x7F8u, kXorMask);
+  o.y = __builtin_amdgcn_bitop3_b32(t1.y, t2.y, 0x7F8u, kXorMask);
+  o.x = __builtin_amdgcn_bitop3_b32(o.x, y.x, 0x788u, kXorAnd);
+  o.y = __builtin_amdgcn_bitop3_b32(o.y, y.y, 0x788u, kXorAnd);
+  return o;
+#else
   t = shl64<15>(y);
   y.x = __builtin_amdgcn_bitop3_b32(y.x, t.x, 0xefc60000u, kXorAnd);
   y.y = __builtin_amdgcn_bitop3_b32(y.y, t.y, 0xefc60000u, kXorAnd);
@@ -628,6 +702,7 @@ __device__ __forceinline__ u32x2_t temper_pair_u8x8(u32x2_t y) {
   o.x = __builtin_amdgcn_bitop3_b32(t1.x, t2.x, 0x7F8u, kXorMask);
   o.y = __builtin_amdgcn_bitop3_b32(t1.y, t2.y, 0x7F8u, kXorMask);
   return o;
+#endif
 }
 
 // bf16 Box-Muller pair before the final rounding: (R[a] * C[b], R[a] * S[b]) + 0 as ONE
@@ -646,6 +721,10 @@ __device__ __forceinline__ f32x2_t z_pair_bf16_raw(uint32_t r1, uint32_t r2) {
 #if FKS_DIAG >= 3  // diagnostics: no table lookups (wrong values)
   const f32x2_t rr = {__uint_as_float(a8 | 0x3f800000u), __uint_as_float(a8 | 0x3f800000u)};
   const f32x2_t cs = {__uint_as_float(b8 | 0x3f000000u), __uint_as_float(b8 | 0x3e000000u)};
+#elif FKS_RPAIR == 2
+  const float r = lds_f32(a8);  // (R,R) entries read as one dword at the x8 index: no shift
+  const f32x2_t rr = {r, r};
+  const f32x2_t cs = lds_f32x2(kLdsCsOff + b8);
 #elif FKS_RPAIR
   const f32x2_t rr = lds_f32x2(a8);
   const f32x2_t cs = lds_f32x2(kLdsCsOff + b8);
@@ -974,6 +1053,309 @@ __global__ __launch_bounds__(DB ? kDbThreads : kApplyThreads,
 #endif
 }
 
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4_t lds_u4_t;
+__device__ __forceinline__ u32x4_t lds_u4(uint32_t off) { return *(const lds_u4_t*)(size_t)off; }
+__device__ __forceinline__ void lds_st4(uint32_t off, u32x4_t v) { *(lds_u4_t*)(size_t)off = v; }
+
+// ------------------------------------------------------------------ small-K kernel v2
+// Table layouts of the small-K kernel's bf16 z (FKS_SM2_TAB): 0 = R f32[256] | (C,S)
+// f32x2[256] (one ds_read_b64 per pair, as the other kernels); 1 = R | C | S as three
+// f32[256] tables read at one x4 index (C and S with one ds_read2st64_b32); 2 = R |
+// (C,S) packed as two bf16 in one dword (ds_read_b32 + two unpack ops).  A random
+// 8-bit-indexed ds_read_b64 costs ~2.7x a ds_read_b32 in LDS cycles (tools/ubench/issue2),
+// and the small-K kernel shares its LDS pipe between 32 waves per CU.
+// x4-scaled folded tempering index of a word pair: ((y << 2) ^ (y >> 16)) & 0x3FC ^
+// ((y >> 1) & 0x3C4) on the second step's y (tests/test_temper_fold.py)
+__device__ __forceinline__ u32x2_t temper_pair_u8x4(u32x2_t y) {
+  u32x2_t t = shr64<11>(y);
+  y.x = __builtin_amdgcn_bitop3_b32(y.x, t.x, 0x001FFFFFu, kXorAnd);
+  y.y ^= t.y;
+  t = shl64<7>(y);
+  y.x = __builtin_amdgcn_bitop3_b32(y.x, t.x, 0x9d2c5680u, kXorAnd);
+  y.y = __builtin_amdgcn_bitop3_b32(y.y, t.y, 0x9d2c5680u, kXorAnd);
+  const u32x2_t t1 = shl64<2>(y), t2 = shr64<16>(y), t3 = shr64<1>(y);
+  u32x2_t o;
+  o.x = __builtin_amdgcn_bitop3_b32(t1.x, t2.x, 0x3FCu, kXorMask);
+  o.y = __builtin_amdgcn_bitop3_b32(t1.y, t2.y, 0x3FCu, kXorMask);
+  o.x = __builtin_amdgcn_bitop3_b32(o.x, t3.x, 0x3C4u, kXorAnd);
+  o.y = __builtin_amdgcn_bitop3_b32(o.y, t3.y, 0x3C4u, kXorAnd);
+  return o;
+}
+
+template <int DT>
+__device__ __forceinline__ f32x2_t z_pair_sm2(const uint8_t* lds, uint32_t r1, uint32_t r2) {
+  if constexpr (DT != FKS_BF16 || FKS_SM2_TAB == 0) {
+    return z_pair2<DT>(lds, r1, r2);
+  } else {
+    u32x2_t w;
+    w.x = r1;
+    w.y = r2;
+    const u32x2_t ab = temper_pair_u8x4(w);
+    const float r = lds_f32(ab.x);
+    f32x2_t cs;
+    if constexpr (FKS_SM2_TAB == 1) {
+      cs.x = lds_f32(1024 + ab.y);
+      cs.y = lds_f32(2048 + ab.y);
+    } else {
+      const uint32_t v = lds_u32(1024 + ab.y);
+      cs.x = __uint_as_float(v << 16);
+      cs.y = __uint_as_float(v & 0xffff0000u);
+    }
+    const f32x2_t rr = {r, r}, zero = {0.0f, 0.0f};
+    return rnd2<DT>(__builtin_elementwise_fma(rr, cs, zero));
+  }
+}
+
+// fks_small2_kernel<DT, MODE>: passes of <= kSmallK seeds over fast segments (the ZO
+// step's perturb / restore + update / K=1 update, optimizer.py:152-173, :146-148).
+// 3 pair waves + 1 twist wave per chunk.  Pair lane q < 156 owns TWO Box-Muller pairs of
+// every block, (j, j+8) and (j+1, j+9) with j = 16 (q/4) + 2 (q%4):
+//   * the four raw words are adjacent in the permuted window (wperm): one ds_read_b128
+//     per seed;
+//   * the four parameters are two aligned element pairs (j, j+1) and (j+8, j+9): two
+//     dword (bf16) / dwordx2 (f32) accesses, no exchange between lanes.
+// The twist wave twists every window of block b+1 out of place while the pair waves
+// run block b (double-buffered windows, one barrier per block).  Window k of buffer B
+// sits at window slot 2k + B and the loops are unrolled by two blocks, so every LDS
+// offset of a block is an immediate.
+// Segment walk: a block lying inside one segment (all but a few hundred blocks of a
+// model) is addressed from a WAVE-UNIFORM base (scalar registers: segment cursor, block
+// range, base address and the segment's scalars) plus the lane's fixed byte offset, so
+// it costs no vector instruction; a block that straddles segments or a gap takes a
+// per-lane path (segment scan, no prefetch).  Lanes q >= 156 mirror lane 155 (same
+// loads, same values stored to the same addresses).
+constexpr int kSm2Threads = 256;
+constexpr int kSm2PairLanes = kMtN / 4;  // 156
+constexpr int kSm2TwistWave = 3;
+
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+  return (uint64_t)rfl((uint32_t)v) | ((uint64_t)rfl((uint32_t)(v >> 32)) << 32);
+}
+__device__ __forceinline__ float rflf(float v) { return __uint_as_float(rfl(__float_as_uint(v))); }
+
+template <int DT, int MODE>
+__global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_kernel(ApplyArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
+  if ((uint32_t)(size_t)(lds_u32_t*)lds32 != 0u) __builtin_trap();
+  const int tid = threadIdx.x;
+  const int c = blockIdx.x;
+  const int nseeds = a.nseeds;
+  const int64_t b0 = a.chunk_block[c];
+  const int nblk = (int)(a.chunk_block[c + 1] - b0);  // host: a chunk is far below 2^31 blocks
+
+  if constexpr (DT == FKS_BF16) {
+    for (int i = tid; i < 256; i += kSm2Threads) {
+      if (FKS_SM2_TAB == 1) {
+        reinterpret_cast<float*>(lds)[i] = c_tab_bf16[i];
+        reinterpret_cast<float*>(lds + 1024)[i] = c_tab_bf16[256 + i];
+        reinterpret_cast<float*>(lds + 2048)[i] = c_tab_bf16[512 + i];
+      } else if (FKS_SM2_TAB == 2) {  // C, S are bf16-exact: (C bits >> 16) | (S bits & 0xffff0000)
+        reinterpret_cast<float*>(lds)[i] = c_tab_bf16[i];
+        reinterpret_cast<uint32_t*>(lds + 1024)[i] =
+            (__float_as_uint(c_tab_bf16[256 + i]) >> 16) | (__float_as_uint(c_tab_bf16[512 + i]) & 0xffff0000u);
+      } else {
+        if (FKS_RPAIR) reinterpret_cast<float2*>(lds)[i] = make_float2(c_tab_bf16[i], c_tab_bf16[i]);
+        else reinterpret_cast<float*>(lds)[i] = c_tab_bf16[i];
+        reinterpret_cast<float2*>(lds + kLdsCsOff)[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
+      }
+    }
+  }
+  // the chunk-start windows go to buffer 1, twisted into buffer 0 for block b0
+  for (int idx = tid; idx < nseeds * kMtN; idx += kSm2Threads) {
+    const int k = idx / kMtN, i = idx - k * kMtN;
+    lds_st(kLdsTabBytes + (2 * k + 1) * kWinBytes + 4 * wperm(i), a.states[((size_t)k * a.nchunks + c) * kMtN + i]);
+  }
+  TwistPlan plan;
+  twist_plan(plan, tid, kLdsTabBytes);
+  // FKS_SM2_ROT: the twist role moves to wave (3 + c) % 4 of workgroup c, so the twist
+  // waves of the CU's workgroups do not all sit on the same SIMD when the dispatcher
+  // places wave w of every workgroup alike; vw is the wave's role index
+  const int vw = FKS_SM2_ROT ? (plan.wave - (c & 3)) & 3 : plan.wave;
+  __syncthreads();
+  if (vw == kSm2TwistWave) {
+    auto twist_into = [&](auto dst_c) __attribute__((always_inline)) {
+      constexpr int D = decltype(dst_c)::value;
+#pragma unroll
+      for (int k = 0; k < kSmallK; k++)
+        if (k < nseeds) {
+          if (FKS_SM2_TWREG) twist_oop_reg(plan, (2 * k + 1 - D) * kWinBytes, (2 * k + D) * kWinBytes);
+          else twist_oop(plan, (2 * k + 1 - D) * kWinBytes, (2 * k + D) * kWinBytes);
+        }
+    };
+    if (nblk > 0) twist_into(std::integral_constant<int, 0>{});
+    __syncthreads();
+    for (int t = 0; t < nblk; t += 2) {
+      if (t + 1 < nblk && FKS_DIAG != 2) twist_into(std::integral_constant<int, 1>{});
+      __syncthreads();  // block t+1 is in buffer 1; block t's buffer 0 is free
+      if (t + 1 >= nblk) break;
+      if (t + 2 < nblk && FKS_DIAG != 2) twist_into(std::integral_constant<int, 0>{});
+      __syncthreads();
+    }
+    return;
+  }
+  __syncthreads();  // block b0 is in buffer 0
+
+  const int vt = 64 * vw + (tid & 63);
+  const int q = vt < kSm2PairLanes ? vt : kSm2PairLanes - 1;
+  const int j = 16 * (q >> 2) + 2 * (q & 3);
+  const uint32_t st_off = kLdsTabBytes + 4 * wperm(j);  // words (j, j+8, j+1, j+9), 16-byte aligned
+  float gk[kSmallK];
+#pragma unroll
+  for (int k = 0; k < kSmallK; k++) gk[k] = rflf(k < nseeds ? a.g[k] : 0.0f);
+
+  using ST = Traits<MODE == kModeDelta ? FKS_F32 : DT>;
+  constexpr int kEs = (DT == FKS_F32 || MODE == kModeDelta) ? 4 : 2;
+  constexpr uint32_t kBlockBytes = kMtN * kEs;
+  typedef typename ST::Pair Pair;
+  const uint32_t joff = (uint32_t)j * kEs;
+
+  // wave-uniform segment cursor; block t of the chunk (t relative to b0) is fast when
+  // t in [fb, eb): it starts at or after the segment's start and ends within it
+  int cur = 0;
+  {
+    const int64_t s0 = (int64_t)kMtN * b0;
+    int lo = 0, hi = a.nsegs;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      const DevSeg& sm = a.segs[mid];
+      if ((int64_t)rfl64((uint64_t)(sm.start + sm.numel)) <= s0) lo = mid + 1; else hi = mid;
+    }
+    cur = lo;
+  }
+  int fb = 0, eb = 0, nb = 0;
+  uint64_t base0 = 0;
+  float u_lr = 0.0f, u_wd = 0.0f, u_ps = 0.0f;
+  bool u_wdf = false;
+  auto load_seg = [&]() __attribute__((always_inline)) {
+    if (cur < a.nsegs) {
+      const DevSeg& sg = a.segs[cur];
+      const int64_t st = (int64_t)rfl64((uint64_t)sg.start);
+      const int64_t en = st + (int64_t)rfl64((uint64_t)sg.numel);
+      const int64_t lim = (int64_t)nblk + 1;
+      auto rel = [&](int64_t blk) __attribute__((always_inline)) -> int { const int64_t r = blk - b0; return (int)(r < -1 ? -1 : (r > lim ? lim : r)); };
+      fb = rel((st + kMtN - 1) / kMtN);
+      eb = rel(en / kMtN);
+      nb = rel((en + kMtN - 1) / kMtN);
+      base0 = rfl64(sg.ptr) + (uint64_t)((int64_t)kMtN * b0 - st) * kEs;
+      u_lr = rflf(sg.lr);
+      u_wd = rflf(sg.wd);
+      u_ps = rflf(sg.ps);
+      u_wdf = (rfl(sg.flags) & FKS_HAS_WD) != 0;
+    } else {
+      fb = eb = 0;
+      nb = INT32_MAX;
+    }
+  };
+  load_seg();
+
+  // (cur at fetch time: the first segment ending after block t's start, where a
+  // straddling block's lanes start their scan; fetching block t+1 may move cur on)
+  struct Slot { uint64_t base; int cur; bool fast; Pair r0, r1; };
+  auto fetch = [&](int t) __attribute__((always_inline)) -> Slot {
+    Slot sl;
+    while (t >= nb) { cur++; load_seg(); }
+    sl.cur = cur;
+    sl.fast = t >= fb && t < eb;
+    // a block that is not fast prefetches from the sink (4 KB, any lane's offset fits):
+    // the loads stay unconditional, so no register is reset under a pending load
+    sl.base = sl.fast ? base0 + (uint64_t)(uint32_t)t * kBlockBytes : (uint64_t)(uintptr_t)a.sink;
+    if (MODE != kModeWriteZ) {
+      sl.r0 = ST::load_pair(sl.base + joff);
+      sl.r1 = ST::load_pair(sl.base + joff + 8 * kEs);
+    } else {
+      sl.r0 = 0;
+      sl.r1 = 0;
+    }
+    return sl;
+  };
+
+  // the block's four parameters through every seed of the pass, in seed order
+  auto run = [&](auto buf_c, Pair& r0, Pair& r1, float lr, float wd, bool wdf, float ps) __attribute__((always_inline)) {
+    constexpr int B = decltype(buf_c)::value;
+    // pA = (p_j, p_j+8), pB = (p_j+1, p_j+9): the two Box-Muller pairs' parameters
+    f32x2_t pA = {ST::cvt(ST::lo(r0)), ST::cvt(ST::lo(r1))};
+    f32x2_t pB = {ST::cvt(ST::hi(r0)), ST::cvt(ST::hi(r1))};
+#pragma unroll
+    for (int k = 0; k < kSmallK; k++) {
+      if (k < nseeds) {  // wave-uniform
+        const u32x4_t w = lds_u4(st_off + (uint32_t)((2 * k + B) * kWinBytes));
+        const f32x2_t zA = z_pair_sm2<DT>(lds, w.x, w.y);
+        const f32x2_t zB = z_pair_sm2<DT>(lds, w.z, w.w);
+        pA = apply_pair<DT, MODE>(pA, zA, gk[k], lr, wd, wdf, ps);
+        pB = apply_pair<DT, MODE>(pB, zB, gk[k], lr, wd, wdf, ps);
+      }
+    }
+    if constexpr (sizeof(Pair) == 4) {  // bf16: the high halves of the bf16-exact results
+      r0 = __builtin_amdgcn_perm(__float_as_uint(pB.x), __float_as_uint(pA.x), 0x07060302u);
+      r1 = __builtin_amdgcn_perm(__float_as_uint(pB.y), __float_as_uint(pA.y), 0x07060302u);
+    } else {
+      r0 = ST::pack(ST::bits(pA.x), ST::bits(pB.x));
+      r1 = ST::pack(ST::bits(pA.y), ST::bits(pB.y));
+    }
+  };
+
+  auto block = [&](auto buf_c, Slot& sl, int t) __attribute__((always_inline)) {
+    if (FKS_DIAG != 1) {
+      if (sl.fast) {
+        run(buf_c, sl.r0, sl.r1, u_lr, u_wd, u_wdf, u_ps);
+        ST::store_pair(sl.base + joff, sl.r0);
+        ST::store_pair(sl.base + joff + 8 * kEs, sl.r1);
+      } else {
+        // straddling block: each lane finds its own segment from the cursor on
+        const int64_t s1 = (int64_t)kMtN * (b0 + t) + j;
+        int cc = sl.cur;
+        bool in = false;
+        DevSeg sg;
+        while (cc < a.nsegs) {
+          sg = a.segs[cc];
+          if (s1 < sg.start + sg.numel) { in = s1 >= sg.start; break; }
+          cc++;
+        }
+        if (in) {
+          const uint64_t addr = sg.ptr + (uint64_t)(s1 - sg.start) * kEs;
+          Pair r0 = 0, r1 = 0;
+          if (MODE != kModeWriteZ) {
+            r0 = ST::load_pair(addr);
+            r1 = ST::load_pair(addr + 8 * kEs);
+          }
+          run(buf_c, r0, r1, sg.lr, sg.wd, (sg.flags & FKS_HAS_WD) != 0, sg.ps);
+          ST::store_pair(addr, r0);
+          ST::store_pair(addr + 8 * kEs, r1);
+        }
+      }
+    }
+    __syncthreads();  // the twist wave has block t+1 in place
+  };
+
+#if FKS_SM2_PF == 2
+  // two blocks ahead: block t's slot is refilled with block t+2 right after its stores
+  Slot s0 = fetch(0);
+  Slot s1 = fetch(nblk > 1 ? 1 : 0);
+  for (int t = 0; t < nblk; t += 2) {
+    block(std::integral_constant<int, 0>{}, s0, t);
+    if (t + 1 >= nblk) break;
+    if (t + 2 < nblk) s0 = fetch(t + 2);
+    block(std::integral_constant<int, 1>{}, s1, t + 1);
+    if (t + 3 < nblk) s1 = fetch(t + 3);
+  }
+#else
+  Slot s0 = fetch(0);
+  // a store after the first prefetch, so the loop is entered with the same pending
+  // (load, store) shape as the back edge
+  *reinterpret_cast<volatile uint32_t*>(a.sink + 1) = 0u;
+  for (int t = 0; t < nblk; t += 2) {
+    Slot s1 = fetch(t + 1 < nblk ? t + 1 : t);  // (the last block re-reads itself, unused)
+    block(std::integral_constant<int, 0>{}, s0, t);
+    if (t + 1 >= nblk) break;
+    s0 = fetch(t + 2 < nblk ? t + 2 : t + 1);
+    block(std::integral_constant<int, 1>{}, s1, t + 1);
+  }
+#endif
+}
+
 // ------------------------------------------------------------------ bf16 slice kernel
 // fks_apply_bs_kernel<MODE>: the bf16 fast segments of a reconstruct, 32 seeds per
 // pass, generator state BIT-SLICED (fks_bitslice.h).  One workgroup per CU, two
@@ -1003,10 +1385,6 @@ constexpr int kBsTabBytes = 256 * 4 + 256 * kBsCsBytes;  // 2,048 (3,072)
 constexpr int kBsLdsBytes = kBsTabBytes + 2 * kBsStateBytes;  // 162,816 <= 163,840
 static_assert(kBsLdsBytes <= 163840, "slice kernel LDS");
 
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) u32x4_t lds_u4_t;
-__device__ __forceinline__ u32x4_t lds_u4(uint32_t off) { return *(const lds_u4_t*)(size_t)off; }
-__device__ __forceinline__ void lds_st4(uint32_t off, u32x4_t v) { *(lds_u4_t*)(size_t)off = v; }
 
 // the 32 planes of row i (row byte address ra = state base + 16 i)
 __device__ __forceinline__ void bs_load_row(uint32_t ra, uint32_t (&x)[32]) {
@@ -1642,8 +2020,21 @@ static int launch_apply_f(const ApplyArgs& a, void* stream) {
 }
 
 template <int DT, int MODE>
+static int launch_small2(const ApplyArgs& a, void* stream) {
+  const size_t lds = (size_t)kLdsTabBytes + (size_t)(2 * a.nseeds + 1) * kWinBytes;
+  static PerDevice attr;
+  // the attribute is set once per device: for the largest pass this kernel takes
+  constexpr int kMaxLds = kLdsTabBytes + (2 * kSmallK + 1) * kWinBytes;
+  if (int e = ensure_lds_attr(attr, &fks_small2_kernel<DT, MODE>, kMaxLds)) return e;
+  hipLaunchKernelGGL((fks_small2_kernel<DT, MODE>), dim3((unsigned)a.nchunks), dim3(kSm2Threads), lds,
+                     (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+template <int DT, int MODE>
 static int launch_apply_t(const ApplyArgs& a, void* stream) {
   if (a.nseeds == kMaxSeedsPerPass) return launch_apply_f<DT, MODE, true>(a, stream);
+  if (FKS_SMALL_V2 && a.nseeds <= kSmallK && DT != FKS_F16) return launch_small2<DT == FKS_F16 ? FKS_F32 : DT, MODE>(a, stream);
   if (FKS_SMALL_DBUF && a.nseeds <= kSmallK) return launch_apply_f<DT, MODE, false, true>(a, stream);
   return launch_apply_f<DT, MODE, false>(a, stream);
 }

@@ -92,11 +92,16 @@ constexpr int kApplyWgPerCu = FKS_APPLY_WG_PER_CU;  // resident apply workgroups
 constexpr int kMaxSeedsPerPass = (160 * 1024 / kApplyWgPerCu - 4096) / 2496 - 1;  // tables: <= 4 KB
 // calls of at most kSmallK seeds run one pass over kSmallWgPerCu workgroups per CU
 constexpr int kSmallK = 4;
-#ifndef FKS_SMALL_WG_PER_CU
-#define FKS_SMALL_WG_PER_CU 5
+#ifndef FKS_SMALL_V2
+#define FKS_SMALL_V2 1  // passes of <= kSmallK seeds over fast segments: fks_small2_kernel (two pairs per lane)
 #endif
-// partial-pass variants take 62-68 VGPRs (7 waves/SIMD): 5 workgroups of 5 waves fit;
-// measured per K=1 pass over the 7B layout: 4 WGs 14.5 ms, 5 WGs 12.9 ms, 6 WGs 18.6 ms
+#ifndef FKS_SMALL_WG_PER_CU
+#define FKS_SMALL_WG_PER_CU (FKS_SMALL_V2 ? 8 : 5)
+#endif
+// v1 (FKS_SMALL_V2=0): 62-68 VGPRs (7 waves/SIMD), 5 workgroups of 5 waves; measured per
+// K=1 pass over the 7B layout: 4 WGs 14.5 ms, 5 WGs 12.9 ms, 6 WGs 18.6 ms.
+// v2: 56 VGPRs, 8 workgroups of 4 waves (8 waves/SIMD; K = 1, 2 fit 8 in LDS, K = 4 six):
+// perturb 7.2 ms at 8 WGs, 7.8 ms at 6 (profiles/r02_smallk_ab.log)
 constexpr int kSmallWgPerCu = FKS_SMALL_WG_PER_CU;
 constexpr int kJumpThreads = 1024;  // 16 waves, one chunk's jump per wave at a time
 constexpr int kJumpXLen = 19937 + 624;  // x[0..20560]: y[i + w] = x[i + w + 1], i < 19937, w < 624
@@ -120,7 +125,7 @@ struct ApplyArgs {
   float g[kMaxSeedsPerPass];    // update multiplier per seed (mode 0) / delta coefficient
   const DevSeg* segs;           // regular segments of this launch's dtype, sorted by start
   const int64_t* chunk_block;   // [nchunks + 1] first MT block of each chunk
-  uint64_t* sink;               // 16 bytes of workspace: loads/stores of idle lanes
+  uint64_t* sink;               // 4 KB of workspace: loads/stores of idle lanes (>= one block of f32 pairs)
   int32_t nsegs;
   int32_t nchunks;
   int32_t nseeds;
