@@ -613,7 +613,7 @@ void clear_plan_cache() {
 
 void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* values, int k, int value_kind, int mode,
          void* workspace, size_t ws_bytes, void* stream, const double* tensor_scales = nullptr, int shard = 0,
-         int nshards = 1, uint64_t delta_base = 0) {
+         int nshards = 1, uint64_t delta_base = 0, const float* gdev = nullptr) {
   validate(t, nt);
   if (nshards < 1 || shard < 0 || shard >= nshards) throw Error(-FKS_EINVAL, "bad shard");
   if (k < 0 || (k > 0 && (!seeds || !values))) throw Error(-FKS_EINVAL, "bad seed/value arrays");
@@ -690,6 +690,7 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
         aa.segs = reinterpret_cast<const DevSeg*>(hdr + C->seg_off[d]);
         aa.chunk_block = ja.chunk_block;
         aa.sink = reinterpret_cast<uint64_t*>(ws);
+        aa.gdev = gdev;
         aa.nsegs = C->nsegs[d];
         aa.nchunks = C->Z.reg_chunks;
         aa.nseeds = nb;
@@ -714,6 +715,7 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
       ia.tiny = reinterpret_cast<const DevTiny*>(hdr + C->H.off_tiny);
       ia.chunk_lo = ja.chunk_block;
       ia.chunk_hi = reinterpret_cast<const int64_t*>(hdr + C->H.off_ihi);
+      ia.gdev = gdev;
       ia.nruns = C->Z.nruns;
       ia.ntiny = C->Z.ntiny;
       ia.nchunks = C->Z.irr_chunks;
@@ -924,6 +926,16 @@ int fks_perturb_step(const fks_tensor* t, int32_t nt, uint64_t seed, const doubl
     if (nt > 0 && !scales) throw Error(-FKS_EINVAL, "null scales");
     run(t, nt, &seed, &value, 1, value_kind, update ? kModePerturbUpdate : kModePerturb, workspace, ws_bytes, stream,
         scales);
+  });
+}
+
+int fks_perturb_step_dev(const fks_tensor* t, int32_t nt, uint64_t seed, const double* scales, const float* dev_value,
+                         void* workspace, size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    if (nt > 0 && (!scales || !dev_value)) throw Error(-FKS_EINVAL, "null scales or device value");
+    const double unused = 0.0;
+    run(t, nt, &seed, &unused, 1, FKS_VALUE_TENSOR, kModePerturbUpdate, workspace, ws_bytes, stream, scales, 0, 1, 0,
+        dev_value);
   });
 }
 

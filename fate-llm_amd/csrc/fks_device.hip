@@ -311,12 +311,12 @@ struct Traits<FKS_F16> {
 // Each statement is one torch op rounded to the parameter dtype (fp32 opmath).
 template <int DT>
 __device__ __forceinline__ float apply_one(float p, float z, float g, float lr, float wd, bool has_wd, int mode,
-                                           float ps) {
+                                           float ps, bool upd = true) {
   using TR = Traits<DT>;
   if (mode == kModeDelta) return __fmaf_rn(g, z, p);   // seed-sharded variant: delta += c_k * z (f32)
   if (mode == kModePerturb || mode == kModePerturbUpdate) {
     p = TR::rnd(p + TR::rnd(ps * z));                  // param.data + scaling_factor * eps * z
-    if (mode == kModePerturb) return p;
+    if (mode == kModePerturb || !upd) return p;         // (upd: the device-side apply decision)
   }
   if (mode == kModeUpdate || mode == kModePerturbUpdate) {
     const float gz = TR::rnd(g * z);                    // directional_derivative_value * z
@@ -325,6 +325,18 @@ __device__ __forceinline__ float apply_one(float p, float z, float g, float lr, 
     return TR::rnd(p - TR::rnd(lr * t));                // param.data - lr * (...)
   }
   return z;
+}
+
+// The directional value of a device-side perturb_step (fks_perturb_step_dev): v[0] = g
+// (f32) rounded to the parameter dtype like a VALUE_TENSOR host value, v[1] != 0 applies
+// the update.  Read once per workgroup, wave-uniform.
+template <int DT>
+__device__ __forceinline__ float dev_value_g(const float* v) {
+  const float g = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v[0])));
+  return DT == FKS_F32 ? g : Traits<DT>::rnd(g);
+}
+__device__ __forceinline__ bool dev_value_apply(const float* v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v[1]))) != 0.0f;
 }
 
 // ------------------------------------------------------------------ jump kernel
@@ -765,14 +777,14 @@ __device__ __forceinline__ f32x2_t rnd2(f32x2_t x) {
 
 template <int DT, int MODE>
 __device__ __forceinline__ f32x2_t apply_pair(f32x2_t p, f32x2_t z, float g, float lr, float wd, bool has_wd,
-                                              float ps) {
+                                              float ps, bool upd = true) {
   if (MODE == kModeDelta) {  // delta += c_k * z: one v_pk_fma_f32 per element pair and seed
     const f32x2_t gg = {g, g};
     return __builtin_elementwise_fma(gg, z, p);
   }
   if (MODE == kModePerturb || MODE == kModePerturbUpdate) {
     p = rnd2<DT>(p + rnd2<DT>(ps * z));
-    if (MODE == kModePerturb) return p;
+    if (MODE == kModePerturb || !upd) return p;
   }
   if (MODE == kModeUpdate || MODE == kModeUpdateWd || MODE == kModeUpdateNoWd || MODE == kModePerturbUpdate) {
     const f32x2_t gz = rnd2<DT>(g * z);
@@ -864,11 +876,11 @@ __device__ __forceinline__ void pair_all(const uint8_t* lds, int st_off, const f
 // one seed (partial passes)
 template <int DT, int MODE>
 __device__ __forceinline__ void pair_one(const uint8_t* lds, int st_off, int k, float g, float lr, float wd,
-                                         bool has_wd, float ps, float& p1, float& p2) {
+                                         bool has_wd, float ps, float& p1, float& p2, bool upd = true) {
   const uint64_t w = lds_u64(st_off + k * kWinBytes);
   const f32x2_t z = z_pair2<DT>(lds, (uint32_t)w, (uint32_t)(w >> 32));
   f32x2_t p = {p1, p2};
-  p = apply_pair<DT, MODE>(p, z, g, lr, wd, has_wd, ps);
+  p = apply_pair<DT, MODE>(p, z, g, lr, wd, has_wd, ps, upd);
   p1 = p.x;
   p2 = p.y;
 }
@@ -912,6 +924,13 @@ __global__ __launch_bounds__(DB ? kDbThreads : kApplyThreads,
 #pragma unroll
   for (int k = 0; k < kMaxSeedsPerPass; k++)
     gk[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(k < nseeds ? a.g[k] : 0.0f)));
+  // a device-side perturb_step (one seed): g and the apply decision from device memory
+  bool upd = true;
+  float g0 = gk[0];
+  if (MODE == kModePerturbUpdate && a.gdev) {
+    g0 = dev_value_g<DT == FKS_F16 ? FKS_F16 : DT>(a.gdev);
+    upd = dev_value_apply(a.gdev);
+  }
   __syncthreads();
   // DB: window tw is twisted by wave kWaves - tw (window 0 by the sixth, twist-only wave)
   const int tw = kWaves - plan.wave;
@@ -1020,7 +1039,8 @@ __global__ __launch_bounds__(DB ? kDbThreads : kApplyThreads,
         // a.g[k] straight from the kernel-argument segment (one s_load per seed): a
         // dynamically indexed gk[] would be copied to VGPRs and indexed per seed
         for (int k = 0; k < nseeds; k++)
-          pair_one<DT, MODE>(lds, st_off + buf, k, a.g[k], sl.lr, sl.wd, sl.wdf != 0, sl.ps, p1, p2);
+          pair_one<DT, MODE>(lds, st_off + buf, k, MODE == kModePerturbUpdate ? g0 : a.g[k], sl.lr, sl.wd,
+                             sl.wdf != 0, sl.ps, p1, p2, upd);
       }
       const uint32_t b1v = ST::bits(p1), b2v = ST::bits(p2);
       const uint32_t back = swap_adjacent(odd ? b1v : b2v);  // even gets partner's p1, odd partner's p2
@@ -1205,6 +1225,11 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
   float gk[kSmallK];
 #pragma unroll
   for (int k = 0; k < kSmallK; k++) gk[k] = rflf(k < nseeds ? a.g[k] : 0.0f);
+  bool upd = true;  // a device-side perturb_step: g and the apply decision from device memory
+  if (MODE == kModePerturbUpdate && a.gdev) {
+    gk[0] = dev_value_g<DT>(a.gdev);
+    upd = dev_value_apply(a.gdev);
+  }
 
   using ST = Traits<MODE == kModeDelta ? FKS_F32 : DT>;
   constexpr int kEs = (DT == FKS_F32 || MODE == kModeDelta) ? 4 : 2;
@@ -1284,8 +1309,8 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
         const u32x4_t w = lds_u4(st_off + (uint32_t)((2 * k + B) * kWinBytes));
         const f32x2_t zA = z_pair_sm2<DT>(lds, w.x, w.y);
         const f32x2_t zB = z_pair_sm2<DT>(lds, w.z, w.w);
-        pA = apply_pair<DT, MODE>(pA, zA, gk[k], lr, wd, wdf, ps);
-        pB = apply_pair<DT, MODE>(pB, zB, gk[k], lr, wd, wdf, ps);
+        pA = apply_pair<DT, MODE>(pA, zA, gk[k], lr, wd, wdf, ps, upd);
+        pB = apply_pair<DT, MODE>(pB, zB, gk[k], lr, wd, wdf, ps, upd);
       }
     }
     if constexpr (sizeof(Pair) == 4) {  // bf16: the high halves of the bf16-exact results
@@ -1776,11 +1801,14 @@ __device__ __forceinline__ void irr_run_lane(const uint8_t* lds, const uint32_t*
   }
   const bool has_wd = (R.flags & FKS_HAS_WD) != 0;
   const float* g = a.g[DT];
+  const bool dv = MODE == kModePerturbUpdate && a.gdev;
+  const bool upd = dv ? dev_value_apply(a.gdev) : true;
   for (int k = 0; k < a.nseeds; k++) {
     float z1, z2;
     irr_z_pair<DT>(lds, win_word(win, k, w1), win_word(win, k, w1 + 8), z1, z2);
-    p1 = apply_one<DT>(p1, z1, g[k], R.lr, R.wd, has_wd, MODE, R.ps);
-    p2 = apply_one<DT>(p2, z2, g[k], R.lr, R.wd, has_wd, MODE, R.ps);
+    const float gv = dv ? dev_value_g<DT>(a.gdev) : g[k];
+    p1 = apply_one<DT>(p1, z1, gv, R.lr, R.wd, has_wd, MODE, R.ps, upd);
+    p2 = apply_one<DT>(p2, z2, gv, R.lr, R.wd, has_wd, MODE, R.ps, upd);
   }
   if (on1) TR::store(R.ptr, e1, p1);
   if (on2) TR::store(R.ptr, e1 + 8, p2);
@@ -1798,6 +1826,8 @@ __device__ __forceinline__ void irr_tiny_lane(const uint32_t* win, const IrrArgs
   const bool has_wd = (T.flags & FKS_HAS_WD) != 0;
   const bool sin_half = (T.flags & kTinySin) != 0;
   const float* g = a.g[DT];
+  const bool dv = MODE == kModePerturbUpdate && a.gdev;
+  const bool upd = dv ? dev_value_apply(a.gdev) : true;
   for (int k = 0; k < a.nseeds; k++) {
     const double u1 = u53(mt_temper(win_word(win, k, w)), mt_temper(win_word(win, k, w + 1)));
     const double u2 = u53(mt_temper(win_word(win, k, w + 2)), mt_temper(win_word(win, k, w + 3)));
@@ -1806,7 +1836,7 @@ __device__ __forceinline__ void irr_tiny_lane(const uint32_t* win, const IrrArgs
     const double v = (sin_half ? r * sin(theta) : r * cos(theta)) * 1.0 + 0.0;
     const float zf = (float)v;  // static_cast<scalar_t>(double): via float for bf16 / f16
     const float z = DT == FKS_F32 ? zf : Traits<DT>::rnd(zf);
-    p = apply_one<DT>(p, z, g[k], T.lr, T.wd, has_wd, MODE, T.ps);
+    p = apply_one<DT>(p, z, dv ? dev_value_g<DT>(a.gdev) : g[k], T.lr, T.wd, has_wd, MODE, T.ps, upd);
   }
   TR::store(T.ptr, 0, p);
 }

@@ -126,6 +126,7 @@ struct ApplyArgs {
   const DevSeg* segs;           // regular segments of this launch's dtype, sorted by start
   const int64_t* chunk_block;   // [nchunks + 1] first MT block of each chunk
   uint64_t* sink;               // 4 KB of workspace: loads/stores of idle lanes (>= one block of f32 pairs)
+  const float* gdev;            // kModePerturbUpdate from device memory: {g, apply} (nullptr: g[] above)
   int32_t nsegs;
   int32_t nchunks;
   int32_t nseeds;
@@ -139,6 +140,7 @@ struct IrrArgs {
   const DevTiny* tiny;          // sorted by word
   const int64_t* chunk_lo;      // [nchunks] chunk c twists MT blocks [chunk_lo[c], chunk_hi[c])
   const int64_t* chunk_hi;
+  const float* gdev;            // kModePerturbUpdate from device memory: {g, apply} (nullptr: g[][] above)
   int32_t nruns;
   int32_t ntiny;
   int32_t nchunks;

@@ -181,6 +181,32 @@ def perturb_step(specs: Sequence[ParamSpec], seed: int, scales: Sequence[float],
         b.finish()
 
 
+def perturb_step_device(specs: Sequence[ParamSpec], seed: int, scales: Sequence[float], value: torch.Tensor,
+                        apply: torch.Tensor) -> None:
+    """``perturb_step`` with ``value`` (g) and ``apply`` (bool) as device tensors read by the
+    kernels when they run: the restore perturbation always, the update iff ``apply`` --
+    no host synchronisation on the losses.  g is rounded to each tensor's dtype like a
+    tensor value of ``perturb_step``."""
+    specs = list(specs)
+    if not specs:
+        return
+    if len(scales) != len(specs):
+        raise ValueError("one scale per tensor")
+    b = _Batch(specs)
+    if b.device is None:
+        return
+    if value.device != b.device or apply.device != b.device:
+        raise ValueError("value and apply must live on the parameters' device")
+    L = N.load()
+    sc = np.ascontiguousarray([float(x) for x in scales], dtype=np.float64)
+    with torch.cuda.device(b.device):
+        dv = torch.stack([value.detach().reshape(()).float(), apply.detach().reshape(()).float()])
+        ws, nbytes = b.workspace(1)
+        N.check(L.fks_perturb_step_dev(ctypes.addressof(b.arr), b.n, _seed_u64(seed), sc.ctypes.data, dv.data_ptr(),
+                                       ws.data_ptr(), nbytes, _stream_handle(b.device)))
+        b.finish()
+
+
 def normal_(tensors: Sequence[torch.Tensor], seed: int, frozen: Optional[Sequence[bool]] = None) -> None:
     """Overwrite every tensor with the z the reference draws for it after manual_seed(seed)."""
     specs = [ParamSpec(t, frozen=bool(frozen[i]) if frozen else False) for i, t in enumerate(tensors)]

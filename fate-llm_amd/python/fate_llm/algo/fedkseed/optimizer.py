@@ -53,8 +53,15 @@ class RandomWalkOptimizer(Optimizer):
 class ZerothOrderOptimizer(RandomWalkOptimizer):
     """Two-point (SPSA / MeZO) estimate of the directional derivative along z."""
 
+    # device_step: when the losses are device tensors on the parameters' device and the
+    # restore and update walk the same tensors, g, the NaN checks and the clip decision
+    # stay on the device and the fused restore + update reads them there
+    # (codec.perturb_step_device): no host synchronisation inside zeroth_order_step
+    device_step = True
+
     def __init__(self, params, lr, eps, weight_decay, grad_clip):
         self.eps = eps
+        self._last_step_on_device = False
         super().__init__(params, lr, weight_decay, grad_clip, dict(eps=eps))
 
     def zeroth_order_step(
@@ -72,6 +79,9 @@ class ZerothOrderOptimizer(RandomWalkOptimizer):
         self.random_perturb_parameters(directional_derivative_seed, scaling_factor=-2.0)
         loss_left = closure()
 
+        self._last_step_on_device = self._on_device(loss_right, loss_left)
+        if self._last_step_on_device:
+            return self._device_tail(directional_derivative_seed, loss_right, loss_left)
         right_nan, left_nan = bool(torch.isnan(loss_right)), bool(torch.isnan(loss_left))
         if right_nan or left_nan:
             self.random_perturb_parameters(directional_derivative_seed, scaling_factor=1.0)
@@ -88,6 +98,28 @@ class ZerothOrderOptimizer(RandomWalkOptimizer):
         scales = [1.0 * group["eps"] for group in self.param_groups for _ in group["params"]]
         codec.perturb_step(specs, directional_derivative_seed, scales, float(g), value_is_tensor=True, update=True)
         return g, loss_right, loss_left
+
+    def _on_device(self, loss_right, loss_left) -> bool:
+        if not (self.device_step and self._fusable()):
+            return False
+        dev = next((p.device for group in self.param_groups for p in group["params"]), None)
+        return (dev is not None and dev.type == "cuda" and all(
+            isinstance(x, torch.Tensor) and x.device == dev and x.numel() == 1 for x in (loss_right, loss_left)))
+
+    def _device_tail(self, seed, loss_right, loss_left):
+        """optimizer.py:136-148 without leaving the device: g = (loss_right - loss_left) /
+        (2 eps) as the reference computes it; the update applies unless a loss is NaN or a
+        positive grad_clip is exceeded; the restore perturbation always.  The returned g is
+        NaN where the reference returns a NaN tensor (a NaN loss or a clipped g)."""
+        g = (loss_right - loss_left) / (2 * self.eps)
+        ok = ~(torch.isnan(loss_right) | torch.isnan(loss_left))
+        if self.grad_clip > 0.0:
+            ok = ok & ~(torch.abs(g) > self.grad_clip)
+        torch.manual_seed(seed)
+        specs = codec.resolve_groups(self.param_groups)
+        scales = [1.0 * group["eps"] for group in self.param_groups for _ in group["params"]]
+        codec.perturb_step_device(specs, seed, scales, g, ok)
+        return torch.where(ok, g, torch.full_like(g, math.nan)), loss_right, loss_left
 
     def _fusable(self) -> bool:
         """restore and update walk the same tensors: no frozen parameter in the groups"""
@@ -115,9 +147,28 @@ class KSeedZerothOrderOptimizer(ZerothOrderOptimizer):
                  lr, eps, weight_decay, grad_clip):
         self.seed_candidate = seed_candidates
         self.seed_probabilities = seed_probabilities
+        self._pending = []  # (seed, device g) of device-side steps, not yet in the history
         self.directional_derivative_history: Mapping[int, List[float]] = {s.item(): [] for s in seed_candidates}
         self.sample_random_generator = torch.Generator()  # unseeded, as in the reference (optimizer.py:190)
         super().__init__(params, lr, eps, weight_decay, grad_clip)
+
+    @property
+    def directional_derivative_history(self) -> Mapping[int, List[float]]:
+        """seed -> the g values recorded for it, in step order (optimizer.py:189, :233).
+        Device-side steps record g lazily: reading the history brings every pending g to
+        the host in one transfer (one synchronisation per read, none per step)."""
+        if self._pending:
+            pend, self._pending = self._pending, []
+            vals = torch.stack([g.reshape(()) for _, g in pend]).tolist()
+            for (seed, _), v in zip(pend, vals):
+                if not math.isnan(v):
+                    self._history[seed].append(v)
+        return self._history
+
+    @directional_derivative_history.setter
+    def directional_derivative_history(self, value) -> None:
+        self._pending = []
+        self._history = value
 
     def sample(self) -> int:
         idx = torch.multinomial(input=self.seed_probabilities, num_samples=1,
@@ -136,6 +187,11 @@ class KSeedZerothOrderOptimizer(ZerothOrderOptimizer):
             raise ValueError("closure must not be None")
         seed = self.sample()
         g, loss_right, loss_left = self.zeroth_order_step(seed, closure)
+        if self._last_step_on_device:
+            # g stays on the device: recorded when the history is read; the returned value
+            # is g where it is NaN, else loss_right (optimizer.py:229-235), as a device tensor
+            self._pending.append((seed, g))
+            return torch.where(torch.isnan(g), g, loss_right)
         if math.isnan(g):
             return g
         self.directional_derivative_history[seed].append(g.item())

@@ -142,6 +142,15 @@ int fks_perturb(const fks_tensor* t, int32_t nt, uint64_t seed, const double* sc
 int fks_perturb_step(const fks_tensor* t, int32_t nt, uint64_t seed, const double* scales, double value,
                      int32_t value_kind, int32_t update, void* workspace, size_t ws_bytes, void* stream);
 
+/* fks_perturb_step with g and the update decision read ON THE DEVICE when the kernels
+ * run, so the caller need not synchronise on the losses (optimizer.py:138-148):
+ * dev_value points to two f32 in device memory, written before this call in `stream`
+ * order: dev_value[0] = g (rounded to each tensor's dtype like a FKS_VALUE_TENSOR value),
+ * dev_value[1] != 0 applies the update; == 0 performs the restore perturbation only (a
+ * NaN loss, optimizer.py:138-141, or a clipped g, :41-42). */
+int fks_perturb_step_dev(const fks_tensor* t, int32_t nt, uint64_t seed, const double* scales, const float* dev_value,
+                         void* workspace, size_t ws_bytes, void* stream);
+
 /* ---- seed-sharded variant (BASELINE config C3) ----
  * The reconstruct loop of ClientTrainer.train_once (fedkseed.py:136-141) applies K
  * seeds in order, p <- p - lr*(g_k*z_k + wd*p), i.e. with a = 1 - lr*wd
