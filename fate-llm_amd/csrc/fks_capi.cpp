@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -456,12 +457,33 @@ struct CachedPlan {
   int wd_mode[3] = {kModeUpdate, kModeUpdate, kModeUpdate};  // kModeUpdateWd / NoWd when uniform
   bool have_reg = false, have_irr = false;
   bool have_bs = false;  // bf16 fast segments with their slice-kernel plan (non-small calls)
+  uint64_t chunk_hash = 0;  // the chunk starts (regular + irregular): what a seed's windows depend on
+};
+
+// Jumped windows of the last one-seed call, per device.  The ZO step makes three calls
+// with the same seed over the same parameters (perturb +eps, perturb -2 eps, restore +
+// update), whose plans differ (the perturbation scales) but whose chunk starts -- and
+// so the jump-ahead windows -- are the same: the second and third calls skip the jump.
+// The windows live in a library-owned buffer; every call that uses it records an event
+// on its stream after its launches, and a call on another stream first makes its stream
+// wait for that event (no host synchronisation), so the earlier jump is visible and no
+// earlier reader is overtaken by a later overwrite.  Guarded by g_cache_mu; freed by
+// fks_plan_cache_clear after a device synchronisation.
+struct WinCache {
+  int device = -1;
+  void* buf = nullptr;
+  size_t bytes = 0;
+  void* stream = nullptr;  // the stream of the last call that used the buffer
+  hipEvent_t done = nullptr;  // recorded on `stream` after that call's launches
+  bool valid = false;
+  uint64_t seed = 0, chunk_hash = 0;
 };
 
 constexpr size_t kPlanCacheEntries = 32;
 std::mutex g_cache_mu;
 std::vector<CachedPlan*> g_cache;
 uint64_t g_cache_clock = 0;
+std::vector<WinCache> g_win;
 
 uint64_t fnv1a(const std::vector<uint8_t>& b) {
   uint64_t h = 1469598103934665603ull;
@@ -548,6 +570,13 @@ CachedPlan* build_plan(const fks_tensor* t, int nt, const double* scales, uint64
   }
   put(C->H.off_runs, L.runs.data(), sizeof(DevRun) * L.runs.size());
   put(C->H.off_tiny, L.tiny.data(), sizeof(DevTiny) * L.tiny.size());
+  {
+    std::vector<uint8_t> ck;
+    for (int64_t b : P.chunk_block) key_put(ck, b);
+    key_put(ck, (int64_t)-1);
+    for (int64_t b : IC.lo) key_put(ck, b);
+    C->chunk_hash = fnv1a(ck);
+  }
   (void)hipGetDevice(&C->device);
   hipError_t e = hipMalloc(&C->dev, std::max<size_t>(C->H.total, 256));
   if (e != hipSuccess) {
@@ -609,6 +638,66 @@ void clear_plan_cache() {
   std::lock_guard<std::mutex> lk(g_cache_mu);
   for (CachedPlan* C : g_cache) free_plan(C);
   g_cache.clear();
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  for (WinCache& W : g_win) {
+    (void)hipSetDevice(W.device);
+    (void)hipDeviceSynchronize();
+    if (W.buf) (void)hipFree(W.buf);
+    if (W.done) (void)hipEventDestroy(W.done);
+  }
+  (void)hipSetDevice(cur);
+  g_win.clear();
+}
+
+// The window cache of the current device for a one-seed call on `stream` needing
+// `bytes` (ordered after the buffer's last user), or nullptr when it cannot be used
+// (FKS_NO_WIN_CACHE set, or no memory: the call then jumps into its workspace).
+WinCache* win_cache(void* stream, size_t bytes) {
+  if (std::getenv("FKS_NO_WIN_CACHE")) return nullptr;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  WinCache* W = nullptr;
+  for (WinCache& w : g_win)
+    if (w.device == dev) W = &w;
+  if (!W) {
+    g_win.emplace_back();
+    W = &g_win.back();
+    W->device = dev;
+    if (hipEventCreateWithFlags(&W->done, hipEventDisableTiming) != hipSuccess) {
+      W->done = nullptr;
+      (void)hipGetLastError();
+    }
+  }
+  if (!W->done) return nullptr;
+  if (W->bytes < bytes) {
+    if (W->buf) {
+      // the last user may still read the old buffer
+      if (hipEventSynchronize(W->done) != hipSuccess) return nullptr;
+      (void)hipFree(W->buf);
+      W->buf = nullptr;
+      W->bytes = 0;
+    }
+    W->valid = false;
+    if (hipMalloc(&W->buf, bytes) != hipSuccess) {
+      W->buf = nullptr;
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    W->bytes = bytes;
+  } else if (W->stream && W->stream != stream) {
+    // another stream used the buffer last: wait (on the device) for its launches
+    if (hipStreamWaitEvent((hipStream_t)stream, W->done, 0) != hipSuccess) return nullptr;
+  }
+  W->stream = stream;
+  return W;
+}
+
+// Chunks per jump workgroup (one chunk per wave, 16 waves, one workgroup per CU by
+// LDS): enough workgroups to cover every CU before packing chunks into fewer groups.
+int jump_chunks_per_wg(int nseeds, int nchunks) {
+  const int per_cu = (int)(((int64_t)nseeds * nchunks + device_cu_count() - 1) / device_cu_count());
+  return std::max(1, std::min({FKS_JUMP_MAX_CPW, per_cu, nchunks}));
 }
 
 void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* values, int k, int value_kind, int mode,
@@ -640,6 +729,24 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
   uint8_t* ws = static_cast<uint8_t*>(workspace);
   const uint8_t* hdr = static_cast<const uint8_t*>(C->dev);
   uint32_t* states = reinterpret_cast<uint32_t*>(ws + kWsStatesOff);
+  // one-seed calls: the regular and irregular windows in the per-device window cache,
+  // jumped only when the seed or the chunk starts changed since the last call
+  uint32_t* reg_states = states;
+  uint32_t* irr_states = states;
+  bool reg_cached = false, irr_cached = false;
+  WinCache* W = nullptr;
+  if (k == 1 && !use_bs) {
+    const size_t reg_words = (size_t)kMtN * (C->have_reg ? C->Z.reg_chunks : 0);
+    const size_t irr_words = (size_t)kMtN * (C->have_irr ? C->Z.irr_chunks : 0);
+    W = win_cache(stream, sizeof(uint32_t) * std::max<size_t>(reg_words + irr_words, 1));
+    if (W) {
+      reg_states = static_cast<uint32_t*>(W->buf);
+      irr_states = reg_states + reg_words;
+      const bool hit = W->valid && W->seed == seeds[0] && W->chunk_hash == C->chunk_hash;
+      reg_cached = irr_cached = hit;
+      W->valid = false;  // until this call's jumps are launched
+    }
+  }
   auto gval = [&](int s, int d) -> float {
     return value_kind == FKS_VALUE_TENSOR ? round_to_dtype(values[s], d) : (float)values[s];
   };
@@ -677,15 +784,14 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
       for (int j = 0; j < nb; j++) ja.seeds[j] = seeds[s0 + j];
       ja.polys = reinterpret_cast<const uint64_t*>(hdr + C->H.off_polys);
       ja.chunk_block = reinterpret_cast<const int64_t*>(hdr + C->H.off_cb);
-      ja.states = states;
+      ja.states = reg_states;
       ja.nchunks = C->Z.reg_chunks;
-      // one chunk per wave when few seeds would leave most CUs idle
-      ja.chunks_per_wg = std::max(1, std::min(nb * C->Z.reg_chunks >= 4096 ? 32 : 16, C->Z.reg_chunks));
-      check(timed(1, stream, [&] { return launch_jump(ja, nb, stream); }), "fks_jump_kernel");
+      ja.chunks_per_wg = jump_chunks_per_wg(nb, C->Z.reg_chunks);
+      if (!reg_cached) check(timed(1, stream, [&] { return launch_jump(ja, nb, stream); }), "fks_jump_kernel");
       for (int d = 0; d < 3; d++) {
         if (!C->nsegs[d] || (use_bs && d == FKS_BF16)) continue;
         ApplyArgs aa{};
-        aa.states = states;
+        aa.states = reg_states;
         for (int j = 0; j < nb; j++) aa.g[j] = gval(s0 + j, d);
         aa.segs = reinterpret_cast<const DevSeg*>(hdr + C->seg_off[d]);
         aa.chunk_block = ja.chunk_block;
@@ -703,12 +809,12 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
       for (int j = 0; j < nb; j++) ja.seeds[j] = seeds[s0 + j];
       ja.polys = reinterpret_cast<const uint64_t*>(hdr + C->H.off_ipolys);
       ja.chunk_block = reinterpret_cast<const int64_t*>(hdr + C->H.off_ilo);
-      ja.states = states;
+      ja.states = irr_states;
       ja.nchunks = C->Z.irr_chunks;
       ja.chunks_per_wg = std::max(1, std::min(32, C->Z.irr_chunks));
-      check(timed(1, stream, [&] { return launch_jump(ja, nb, stream); }), "fks_jump_kernel");
+      if (!irr_cached) check(timed(1, stream, [&] { return launch_jump(ja, nb, stream); }), "fks_jump_kernel");
       IrrArgs ia{};
-      ia.states = states;
+      ia.states = irr_states;
       for (int d = 0; d < 3; d++)
         for (int j = 0; j < nb; j++) ia.g[d][j] = gval(s0 + j, d);
       ia.runs = reinterpret_cast<const DevRun*>(hdr + C->H.off_runs);
@@ -723,6 +829,12 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
       ia.mode = mode;
       check(timed(0, stream, [&] { return launch_irregular(ia, stream); }), "fks_irregular_kernel");
     }
+  }
+  if (W) {  // this call's windows are in the cache (jumped now or reused), stream-ordered
+    W->valid = true;
+    W->seed = seeds[0];
+    W->chunk_hash = C->chunk_hash;
+    if (hipEventRecord(W->done, (hipStream_t)stream) != hipSuccess) throw Error(-FKS_EHIP, "window cache event");
   }
 }
 

@@ -104,6 +104,9 @@ constexpr int kSmallK = 4;
 // perturb 7.2 ms at 8 WGs, 7.8 ms at 6 (profiles/r02_smallk_ab.log)
 constexpr int kSmallWgPerCu = FKS_SMALL_WG_PER_CU;
 constexpr int kJumpThreads = 1024;  // 16 waves, one chunk's jump per wave at a time
+#ifndef FKS_JUMP_MAX_CPW
+#define FKS_JUMP_MAX_CPW 32  // most chunks one jump workgroup takes (fks_capi.cpp jump_chunks_per_wg)
+#endif
 constexpr int kJumpXLen = 19937 + 624;  // x[0..20560]: y[i + w] = x[i + w + 1], i < 19937, w < 624
 
 // kModeUpdateWd / kModeUpdateNoWd: kModeUpdate specialised for a launch whose segments

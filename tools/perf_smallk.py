@@ -1,6 +1,9 @@
 """Small-K cost on the 7B bf16 layout (the ZO local step's perturb / update calls):
 wall time per call (synchronised), device time of the apply and jump kernels, and the
-host-side share.  python tools/perf_smallk.py [--params N] [--reps R]"""
+host-side share.  Every repetition uses a new seed (the jumped-window cache misses);
+"zo_step" is the three calls of one zeroth-order step with one seed (perturb +eps,
+perturb -2 eps, restore + update), where the second and third reuse the windows.
+python tools/perf_smallk.py [--params N] [--reps R]"""
 import argparse
 import json
 import os
@@ -37,17 +40,17 @@ def main():
     scalars = [g if g != 0.0 else 1.0 for g in scalars]
 
     def measure(name, fn):
-        fn()
+        fn(0)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         with codec.profile() as prof:
-            for _ in range(args.reps):
-                fn()
+            for i in range(args.reps):
+                fn(1 + i)
             torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) / args.reps * 1e3
         t1 = time.perf_counter()
-        for _ in range(args.reps):
-            fn()
+        for i in range(args.reps):
+            fn(1 + args.reps + i)
         host = (time.perf_counter() - t1) / args.reps * 1e3  # enqueue only (async)
         torch.cuda.synchronize()
         rec = {"call": name, "wall_ms": round(wall, 3), "apply_ms": round(prof.apply_ms / args.reps, 3),
@@ -55,10 +58,19 @@ def main():
                "GBps": round(total * 2 / wall * 1e-6, 1)}
         print(json.dumps(rec), flush=True)
 
-    measure("perturb", lambda: codec.perturb(views, seeds[0], 5e-4))
-    measure("perturb_step", lambda: codec.perturb_step(specs, seeds[0], [5e-4] * len(specs), 1.5))
+    sd = lambda i: seeds[i % len(seeds)]  # noqa: E731
+
+    def zo_step(i):
+        codec.perturb(views, sd(i), 5e-4)
+        codec.perturb(views, sd(i), -1e-3)
+        codec.perturb_step(specs, sd(i), [5e-4] * len(specs), 1.5)
+
+    measure("perturb", lambda i: codec.perturb(views, sd(i), 5e-4))
+    measure("perturb_step", lambda i: codec.perturb_step(specs, sd(i), [5e-4] * len(specs), 1.5))
+    measure("zo_step (3 calls)", zo_step)
     for k in [int(x) for x in args.ks.split(",")]:
-        measure(f"directional_step K={k}", lambda: codec.directional_step(specs, seeds[:k], scalars[:k]))
+        measure(f"directional_step K={k}",
+                lambda i: codec.directional_step(specs, [sd(i + j) for j in range(k)], scalars[:k]))
 
 
 if __name__ == "__main__":
