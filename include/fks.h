@@ -122,7 +122,13 @@ int fks_profile_end(double* apply_ms, int64_t* n_apply, double* jump_ms, int64_t
  * the device in a bounded LRU plan cache: repeated calls over the same parameters (the
  * optimizer's perturb / update calls, repeated reconstructs) do no host-side layout
  * work and no upload.  fks_plan_cache_clear synchronises the device and frees every
- * cached header (e.g. before freeing the parameters' memory pool). */
+ * cached header (e.g. before freeing the parameters' memory pool).
+ *
+ * One-seed calls (perturb, perturb_step, a K=1 update) keep the generator windows they
+ * jumped to in a library-owned per-device buffer, keyed by the seed and the chunk starts:
+ * the zeroth-order step's three calls with one seed over one parameter list jump once.
+ * Use across streams is ordered by an event (no host synchronisation); the buffer is
+ * freed by fks_plan_cache_clear; FKS_NO_WIN_CACHE in the environment turns it off. */
 int fks_plan_cache_clear(void);
 
 /* torch.manual_seed(seed); for every tensor i in order: p = p + scales[i]*z, where
