@@ -28,11 +28,25 @@ def probability_from_amps(amps: List[List[float]], clip):
     return ((amp - lo) / (hi - lo + 1e-10)).softmax(0)
 
 
-def _value_kind(value):
+def _value_kind(value, specs=()):
+    """(g as a python float, whether it is a tensor): a tensor g is cast to each
+    parameter's dtype by the reference's ``g * z`` (zo_utils.py:49).  A 1-element tensor
+    that is not 0-dim takes part in type promotion and broadcasting as a dimensioned
+    tensor: that is the same update when the promoted dtype is the parameter's own and
+    the parameter has a dimension; otherwise the reference rebinds ``param.data`` to a
+    tensor of another dtype or shape, which an in-place update cannot be -- raised."""
     if isinstance(value, torch.Tensor):
         if value.dim() != 0:
-            raise ValueError("directional_derivative_value must be a python number or a 0-dim tensor")
-        return float(value.item()), True
+            if value.numel() != 1:
+                raise ValueError("directional_derivative_value must be a python number or a 1-element tensor")
+            for sp in specs:
+                t = sp.tensor
+                if torch.promote_types(value.dtype, t.dtype) != t.dtype or t.dim() == 0:
+                    raise NotImplementedError(
+                        f"a {tuple(value.shape)} {value.dtype} directional_derivative_value would turn a "
+                        f"{tuple(t.shape)} {t.dtype} parameter into {torch.promote_types(value.dtype, t.dtype)} "
+                        "of the broadcast shape (the reference rebinds param.data); pass a 0-dim tensor")
+        return float(value.reshape(()).item()), True
     return float(value), False
 
 
@@ -53,7 +67,7 @@ def directional_derivative_step(
     """
     torch.manual_seed(directional_derivative_seed)
     specs = codec.resolve_groups(param_groups, lr=lr, weight_decay=weight_decay)
-    v, is_tensor = _value_kind(directional_derivative_value)
+    v, is_tensor = _value_kind(directional_derivative_value, specs)
     codec.directional_step(specs, [directional_derivative_seed], [v], value_is_tensor=is_tensor)
     return directional_derivative_value
 
