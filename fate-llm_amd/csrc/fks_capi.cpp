@@ -1075,6 +1075,24 @@ int fks_host_jump_window(uint64_t seed, int64_t block, uint32_t* out624) {
   });
 }
 
+int fks_device_selfcheck(int32_t which, uint64_t* result, void* workspace, size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    if (!result || which != FKS_CHECK_SQRT_DOMAIN) throw Error(-FKS_EINVAL, "bad arguments");
+    const size_t need = sizeof(uint32_t) * (size_t)kSqrtDomainBlocks;
+    if (!workspace || ws_bytes < need) throw Error(-FKS_EINVAL, "workspace too small");
+    uint32_t* counts = static_cast<uint32_t*>(workspace);
+    int rc = launch_sqrt_domain_check(counts, stream);
+    if (rc) throw Error(-FKS_EHIP, std::string("sqrt domain check launch: ") + hipGetErrorString((hipError_t)rc));
+    std::vector<uint32_t> h((size_t)kSqrtDomainBlocks);
+    if (hipMemcpyAsync(h.data(), counts, need, hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
+        hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+      throw Error(-FKS_EHIP, "sqrt domain check copy");
+    uint64_t bad = 0;
+    for (uint32_t v : h) bad += v;
+    *result = bad;
+  });
+}
+
 int fks_host_tables(int32_t dtype, float* radius, float* cosv, float* sinv, int32_t n) {
   return guarded([&] {
     const Tables& T = tables();

@@ -80,6 +80,13 @@
 #ifndef FKS_BS_CSPACK
 #define FKS_BS_CSPACK 0  // slice kernel: (C,S) table as packed bf16 pairs (ds_read_b32) instead of f32 pairs (ds_read_b64)
 #endif
+#ifndef FKS_F32_RSQRT
+#define FKS_F32_RSQRT 0  // fp32 radius: 1 = v_sqrt_f32 + one residual step, no denormal scaling
+                         // (fewer instructions, measured 4 % slower: 1.74 vs 1.67 ps per seed*param)
+#endif
+#ifndef FKS_F32_FAST
+#define FKS_F32_FAST 1  // fp32 z: pair tempering and the domain-exact sincos / fma rewrites (z_pair_f32_raw)
+#endif
 #ifndef FKS_TEMPER_FOLD
 #define FKS_TEMPER_FOLD 1  // bf16 pair tempering with the third step folded into the index (temper_pair_u8x8)
 #endif
@@ -717,6 +724,90 @@ __device__ __forceinline__ u32x2_t temper_pair_u8x8(u32x2_t y) {
 #endif
 }
 
+// fp32 z pair from the two RAW words of a 16-block (FKS_F32_FAST): the same values as
+// z_pair_f32(mt_temper(r1), mt_temper(r2)) with fewer instructions, all exact rewrites
+// on this input domain (pinned by the golden fp32 streams):
+//   * both words tempered on the 64-bit pair (masks clear the bits one word shifts into
+//     the other; only the low 24 bits are kept);
+//   * theta = 2*pi*d2 >= +0, so sincos256_ps's sign extraction and abs are identities;
+//   * its select-and-add merge of the two polynomials is a swap (the adds involve an
+//     exact zero; a zero's sign cannot reach z, which is rounded as radius*s + 0);
+//   * radius*c + 0 (mul, then the fmadd with std 1, mean 0) is fma(radius, c, 0): the
+//     exact product is never a nonzero below the subnormal range here.
+__device__ __forceinline__ u32x2_t temper_pair_u24(u32x2_t y) {
+  u32x2_t t = shr64<11>(y);
+  y.x = __builtin_amdgcn_bitop3_b32(y.x, t.x, 0x001FFFFFu, kXorAnd);
+  y.y ^= t.y;
+  t = shl64<7>(y);
+  y.x = __builtin_amdgcn_bitop3_b32(y.x, t.x, 0x9d2c5680u, kXorAnd);
+  y.y = __builtin_amdgcn_bitop3_b32(y.y, t.y, 0x9d2c5680u, kXorAnd);
+  t = shl64<15>(y);
+  y.x = __builtin_amdgcn_bitop3_b32(y.x, t.x, 0xefc60000u, kXorAnd);
+  y.y = __builtin_amdgcn_bitop3_b32(y.y, t.y, 0xefc60000u, kXorAnd);
+  t = shr64<18>(y);
+  y.x = __builtin_amdgcn_bitop3_b32(y.x, t.x, 0x3FFFu, kXorAnd) & 0xFFFFFFu;
+  y.y = __builtin_amdgcn_bitop3_b32(y.y, t.y, 0xFFFFFFu, kXorMask);
+  return y;
+}
+
+__device__ __forceinline__ void cephes_sincosf_nonneg(float x, float& s, float& c) {
+  float y = x * 1.27323954473516f;
+  int32_t imm2 = (int32_t)y;
+  imm2 = (imm2 + 1) & ~1;
+  y = (float)imm2;
+  const uint32_t sign_bit_sin = ((uint32_t)(imm2 & 4)) << 29;
+  const uint32_t sign_bit_cos = ((uint32_t)(~(imm2 - 2) & 4)) << 29;
+  const bool poly_mask = (imm2 & 2) == 0;
+  x = __fmaf_rn(y, -0.78515625f, x);
+  x = __fmaf_rn(y, -2.4187564849853515625e-4f, x);
+  x = __fmaf_rn(y, -3.77489497744594108e-8f, x);
+  const float z = x * x;
+  float yc = 2.443315711809948E-005f;
+  yc = __fmaf_rn(yc, z, -1.388731625493765E-003f);
+  yc = __fmaf_rn(yc, z, 4.166664568298827E-002f);
+  yc = yc * z;
+  yc = __fmaf_rn(yc, z, -(z * 0.5f));
+  yc = yc + 1.0f;
+  float ys = -1.9515295891E-4f;
+  ys = __fmaf_rn(ys, z, 8.3321608736E-3f);
+  ys = __fmaf_rn(ys, z, -1.6666654611E-1f);
+  ys = ys * z;
+  ys = __fmaf_rn(ys, x, x);
+  const float xmm1 = poly_mask ? ys : yc;
+  const float xmm2 = poly_mask ? yc : ys;
+  s = __uint_as_float(__float_as_uint(xmm1) ^ sign_bit_sin);
+  c = __uint_as_float(__float_as_uint(xmm2) ^ sign_bit_cos);
+}
+
+// Correctly rounded sqrt of the radius input x = -2 log(u1), as _mm256_sqrt_ps: the
+// compiler's expansion, or (FKS_F32_RSQRT) v_sqrt_f32 -- NOT correctly rounded on this
+// domain by itself -- and one residual step to the neighbour, without the generic
+// denormal scaling (x is +-0 or >= 2^-23).  Either is checked on all 2^24 inputs against
+// the exact midpoint criterion (fks_device_selfcheck FKS_CHECK_SQRT_DOMAIN, a GPU test).
+__device__ __forceinline__ float radius_sqrt(float x) {
+  if (!FKS_F32_RSQRT) return sqrtf(x);  // the compiler's correctly rounded expansion
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float dn = __int_as_float(__float_as_int(s) - 1), up = __int_as_float(__float_as_int(s) + 1);
+  const float rdn = __fmaf_rn(-dn, s, x), rup = __fmaf_rn(-up, s, x);
+  float r = rdn <= 0.0f ? dn : s;
+  r = rup > 0.0f ? up : r;
+  return x > 0.0f ? r : x;
+}
+
+__device__ __forceinline__ void z_pair_f32_raw(uint32_t r1, uint32_t r2, float& z1, float& z2) {
+  u32x2_t w;
+  w.x = r1;
+  w.y = r2;
+  const u32x2_t t = temper_pair_u24(w);
+  const float d1 = (float)t.x * (1.0f / 16777216.0f);
+  const float d2 = (float)t.y * (1.0f / 16777216.0f);
+  const float radius = radius_sqrt(-2.0f * cephes_logf(1.0f - d1));
+  float s, c;
+  cephes_sincosf_nonneg(6.28318548202514648438f * d2, s, c);
+  z1 = __fmaf_rn(radius, c, 0.0f);
+  z2 = __fmaf_rn(radius, s, 0.0f);
+}
+
 // bf16 Box-Muller pair before the final rounding: (R[a] * C[b], R[a] * S[b]) + 0 as ONE
 // v_pk_fma_f32 (R*C is exact in f32: 8-bit x 8-bit significands; the +0 addend turns
 // -0 into +0 like normal_fill_16's "+ mean").  (R,R) pairs at LDS 0, (C,S) pairs at 2048.
@@ -753,7 +844,8 @@ __device__ __forceinline__ f32x2_t z_pair_bf16_raw(uint32_t r1, uint32_t r2) {
 template <int DT>
 __device__ __forceinline__ void z_pair(const uint8_t* lds, uint32_t r1, uint32_t r2, float& z1, float& z2) {
   if constexpr (DT == FKS_F32) {
-    z_pair_f32(mt_temper(r1), mt_temper(r2), z1, z2);
+    if (FKS_F32_FAST) z_pair_f32_raw(r1, r2, z1, z2);
+    else z_pair_f32(mt_temper(r1), mt_temper(r2), z1, z2);
   } else {
     // normal_fill_16<BFloat16>: z = bf16(R[a] * C[b]) * 1 + 0 (std, mean).  R*C is exact
     // in f32 (8-bit x 8-bit significands) and fma(R, C, +0) turns -0 into +0 like "+ mean".
@@ -2129,6 +2221,38 @@ static int launch_irregular_m(const IrrArgs& a, void* stream) {
   if (int e = ensure_lds_attr(attr, &fks_irregular_kernel<MODE>, (int)lds)) return e;
   hipLaunchKernelGGL((fks_irregular_kernel<MODE>), dim3((unsigned)a.nchunks), dim3(kApplyThreads), lds,
                      (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+// Device self check FKS_CHECK_SQRT_DOMAIN: for every u1 = 1 - k 2^-24 the fp32
+// Box-Muller can draw, x = -2 cephes_logf(u1); counts the k where radius_sqrt(x) is not
+// the correctly rounded square root.  The criterion is exact and uses no square root:
+// s = RN(sqrt(x)) iff m_lo^2 < x < m_hi^2 for the midpoints m to s's neighbours (25-bit
+// values, squared exactly in double; a 24-bit x never equals such a square).  One count
+// per workgroup of 256.
+__global__ __launch_bounds__(256) void fks_sqrt_domain_kernel(uint32_t* counts) {
+  __shared__ uint32_t bad;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+  const float x = -2.0f * cephes_logf(1.0f - (float)k * (1.0f / 16777216.0f));
+  const float s = radius_sqrt(x);
+  bool ok;
+  if (x > 0.0f) {
+    const double sd = (double)s;
+    const double lo = 0.5 * (sd + (double)__int_as_float(__float_as_int(s) - 1));
+    const double hi = 0.5 * (sd + (double)__int_as_float(__float_as_int(s) + 1));
+    ok = lo * lo < (double)x && (double)x < hi * hi;
+  } else {
+    ok = __float_as_uint(s) == __float_as_uint(x);  // sqrt(+-0) = +-0
+  }
+  if (!ok) atomicAdd(&bad, 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) counts[blockIdx.x] = bad;
+}
+
+int launch_sqrt_domain_check(uint32_t* counts, void* stream) {
+  hipLaunchKernelGGL(fks_sqrt_domain_kernel, dim3(kSqrtDomainBlocks), dim3(256), 0, (hipStream_t)stream, counts);
   return (int)hipGetLastError();
 }
 

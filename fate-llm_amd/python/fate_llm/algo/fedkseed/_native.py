@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("FKS_LIB_OVERRIDE") or os.path.join(_HERE, "libfks.so"
 F32, BF16, F16 = 0, 1, 2
 HAS_WD, FROZEN = 1, 2
 VALUE_SCALAR, VALUE_TENSOR = 0, 1
+CHECK_SQRT_DOMAIN = 1
 ABI_VERSION = 1
 
 # every symbol include/fks.h declares (checked by tests/test_capi_host.py)
@@ -24,7 +25,7 @@ EXPORTED = (
     "fks_abi_version", "fks_build_target", "fks_host_jump_window", "fks_host_tables",
     "fks_directional_step_shard", "fks_stream_length", "fks_profile_begin", "fks_profile_end",
     "fks_shard_census", "fks_perturb_step", "fks_delta_workspace_size", "fks_delta_accumulate", "fks_delta_apply",
-    "fks_plan_cache_clear", "fks_perturb_step_dev",
+    "fks_plan_cache_clear", "fks_perturb_step_dev", "fks_device_selfcheck",
 )
 
 
@@ -82,11 +83,12 @@ def load():
         L.fks_delta_apply.argtypes = [P, c_i32, P, P, P, c_sz, P]
         L.fks_plan_cache_clear.argtypes = []
         L.fks_perturb_step_dev.argtypes = [P, c_i32, c_u64, P, P, P, c_sz, P]
+        L.fks_device_selfcheck.argtypes = [c_i32, ctypes.POINTER(c_u64), P, c_sz, P]
         for name in ("fks_workspace_size", "fks_directional_step", "fks_perturb", "fks_normal",
                      "fks_host_jump_window", "fks_host_tables", "fks_directional_step_shard",
                      "fks_stream_length", "fks_profile_begin", "fks_profile_end", "fks_shard_census", "fks_perturb_step",
                      "fks_delta_workspace_size", "fks_delta_accumulate", "fks_delta_apply", "fks_plan_cache_clear",
-                     "fks_perturb_step_dev"):
+                     "fks_perturb_step_dev", "fks_device_selfcheck"):
             getattr(L, name).restype = ctypes.c_int
         if L.fks_abi_version() != ABI_VERSION:
             raise OSError(f"libfks.so ABI {L.fks_abi_version()} != {ABI_VERSION}")

@@ -197,6 +197,14 @@ const char* fks_build_target(void);
 int fks_host_jump_window(uint64_t seed, int64_t block, uint32_t* out624);
 int fks_host_tables(int32_t dtype, float* radius, float* cosv, float* sinv, int32_t n);
 
+/* Device self checks of a property a kernel relies on; *result = number of violations
+ * (0 = holds), synchronous on `stream`.  FKS_CHECK_SQRT_DOMAIN: the fp32 Box-Muller's
+ * radius sqrt(-2 log u1) must be correctly rounded (as _mm256_sqrt_ps is) on all 2^24
+ * values of u1 the reference can draw, checked against the exact midpoint criterion;
+ * workspace >= 262,144 bytes. */
+#define FKS_CHECK_SQRT_DOMAIN 1
+int fks_device_selfcheck(int32_t which, uint64_t* result, void* workspace, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
