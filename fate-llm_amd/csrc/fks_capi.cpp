@@ -458,6 +458,24 @@ struct CachedPlan {
   bool have_reg = false, have_irr = false;
   bool have_bs = false;  // bf16 fast segments with their slice-kernel plan (non-small calls)
   uint64_t chunk_hash = 0;  // the chunk starts (regular + irregular): what a seed's windows depend on
+  int64_t reg_lo = 0, reg_hi = 0;  // MT blocks [reg_lo, reg_hi) the regular chunks cover
+};
+
+// Table indices of the last one-seed bf16 perturb, per device (ZO step: the second and
+// third calls replay them, fks_small2_kernel ZM 2).  A block's indices depend only on
+// the seed and the block's stream position, not on the tensors, so any later one-seed
+// call with the same seed whose regular blocks lie inside the stored range replays them.
+// 1 byte per parameter of device memory; allocated only while it is a small share of the
+// free memory (FKS_ZCACHE=0 turns it off).  Stream hand-off by event, as WinCache.
+struct ZCache {
+  int device = -1;
+  void* buf = nullptr;
+  size_t bytes = 0;
+  void* stream = nullptr;
+  hipEvent_t done = nullptr;
+  bool valid = false;
+  uint64_t seed = 0;
+  int64_t lo = 0, hi = 0;
 };
 
 // Jumped windows of the last one-seed call, per device.  The ZO step makes three calls
@@ -484,6 +502,7 @@ std::mutex g_cache_mu;
 std::vector<CachedPlan*> g_cache;
 uint64_t g_cache_clock = 0;
 std::vector<WinCache> g_win;
+std::vector<ZCache> g_zc;
 
 uint64_t fnv1a(const std::vector<uint8_t>& b) {
   uint64_t h = 1469598103934665603ull;
@@ -577,6 +596,10 @@ CachedPlan* build_plan(const fks_tensor* t, int nt, const double* scales, uint64
     for (int64_t b : IC.lo) key_put(ck, b);
     C->chunk_hash = fnv1a(ck);
   }
+  if (C->have_reg && !P.chunk_block.empty()) {
+    C->reg_lo = P.chunk_block.front();
+    C->reg_hi = P.chunk_block.back();
+  }
   (void)hipGetDevice(&C->device);
   hipError_t e = hipMalloc(&C->dev, std::max<size_t>(C->H.total, 256));
   if (e != hipSuccess) {
@@ -646,8 +669,63 @@ void clear_plan_cache() {
     if (W.buf) (void)hipFree(W.buf);
     if (W.done) (void)hipEventDestroy(W.done);
   }
+  for (ZCache& Z : g_zc) {
+    (void)hipSetDevice(Z.device);
+    (void)hipDeviceSynchronize();
+    if (Z.buf) (void)hipFree(Z.buf);
+    if (Z.done) (void)hipEventDestroy(Z.done);
+  }
   (void)hipSetDevice(cur);
   g_win.clear();
+  g_zc.clear();
+}
+
+// The z-index cache of the current device, ordered after its last user on `stream`,
+// with room for `bytes` (allocated if the free memory allows), or nullptr.
+ZCache* z_cache(void* stream, size_t bytes) {
+  const char* env = std::getenv("FKS_ZCACHE");
+  if (env && env[0] == '0') return nullptr;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  ZCache* Z = nullptr;
+  for (ZCache& z : g_zc)
+    if (z.device == dev) Z = &z;
+  if (!Z) {
+    g_zc.emplace_back();
+    Z = &g_zc.back();
+    Z->device = dev;
+    if (hipEventCreateWithFlags(&Z->done, hipEventDisableTiming) != hipSuccess) {
+      Z->done = nullptr;
+      (void)hipGetLastError();
+    }
+  }
+  if (!Z->done) return nullptr;
+  if (Z->bytes < bytes) {
+    if (Z->buf) {
+      if (hipEventSynchronize(Z->done) != hipSuccess) return nullptr;
+      (void)hipFree(Z->buf);
+      Z->buf = nullptr;
+      Z->bytes = 0;
+    }
+    Z->valid = false;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    // a small share of what is free: the parameters' owner keeps its headroom
+    if (bytes + std::max<size_t>(total_b / 10, (size_t)4 << 30) > free_b) return nullptr;
+    if (hipMalloc(&Z->buf, bytes) != hipSuccess) {
+      Z->buf = nullptr;
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    Z->bytes = bytes;
+  } else if (Z->stream && Z->stream != stream) {
+    if (hipStreamWaitEvent((hipStream_t)stream, Z->done, 0) != hipSuccess) return nullptr;
+  }
+  Z->stream = stream;
+  return Z;
 }
 
 // The window cache of the current device for a one-seed call on `stream` needing
@@ -729,11 +807,31 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
   uint8_t* ws = static_cast<uint8_t*>(workspace);
   const uint8_t* hdr = static_cast<const uint8_t*>(C->dev);
   uint32_t* states = reinterpret_cast<uint32_t*>(ws + kWsStatesOff);
+  // one-seed bf16 calls: store the table indices (a perturb) or replay them (a later call
+  // with the same seed inside the stored block range): ZCache
+  ZCache* Zc = nullptr;
+  int zmode = 0;
+  const bool z_mode_ok = mode == kModePerturb || mode == kModePerturbUpdate || mode == kModeUpdate;
+  if (k == 1 && small && !use_bs && C->have_reg && C->nsegs[FKS_BF16] > 0 && z_mode_ok) {
+    Zc = z_cache(stream, (size_t)kSm2ZidxBytesPerBlock * (size_t)(C->reg_hi - C->reg_lo));
+    if (Zc) {
+      if (Zc->valid && Zc->seed == seeds[0] && Zc->lo <= C->reg_lo && C->reg_hi <= Zc->hi) {
+        zmode = 2;
+      } else if (mode == kModePerturb) {
+        zmode = 1;
+        Zc->valid = false;  // until this call's store is launched
+        Zc->lo = C->reg_lo;
+        Zc->hi = C->reg_hi;
+      } else {
+        Zc = nullptr;
+      }
+    }
+  }
   // one-seed calls: the regular and irregular windows in the per-device window cache,
   // jumped only when the seed or the chunk starts changed since the last call
   uint32_t* reg_states = states;
   uint32_t* irr_states = states;
-  bool reg_cached = false, irr_cached = false;
+  bool reg_cached = false, irr_cached = false, reg_jumped = false;
   WinCache* W = nullptr;
   if (k == 1 && !use_bs) {
     const size_t reg_words = (size_t)kMtN * (C->have_reg ? C->Z.reg_chunks : 0);
@@ -787,7 +885,12 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
       ja.states = reg_states;
       ja.nchunks = C->Z.reg_chunks;
       ja.chunks_per_wg = jump_chunks_per_wg(nb, C->Z.reg_chunks);
-      if (!reg_cached) check(timed(1, stream, [&] { return launch_jump(ja, nb, stream); }), "fks_jump_kernel");
+      // a replay needs no windows unless another dtype's segments still generate
+      const bool need_windows = zmode != 2 || C->nsegs[FKS_F32] > 0 || C->nsegs[FKS_F16] > 0;
+      if (!reg_cached && need_windows) {
+        check(timed(1, stream, [&] { return launch_jump(ja, nb, stream); }), "fks_jump_kernel");
+        reg_jumped = true;
+      }
       for (int d = 0; d < 3; d++) {
         if (!C->nsegs[d] || (use_bs && d == FKS_BF16)) continue;
         ApplyArgs aa{};
@@ -797,6 +900,11 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
         aa.chunk_block = ja.chunk_block;
         aa.sink = reinterpret_cast<uint64_t*>(ws);
         aa.gdev = gdev;
+        if (Zc && d == FKS_BF16) {
+          aa.zidx = static_cast<uint32_t*>(Zc->buf);
+          aa.zlo = Zc->lo;
+          aa.zmode = zmode;
+        }
         aa.nsegs = C->nsegs[d];
         aa.nchunks = C->Z.reg_chunks;
         aa.nseeds = nb;
@@ -831,10 +939,18 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
     }
   }
   if (W) {  // this call's windows are in the cache (jumped now or reused), stream-ordered
-    W->valid = true;
+    // (a replay that skipped the jump did not write the regular windows)
+    W->valid = reg_cached || reg_jumped || !C->have_reg;
     W->seed = seeds[0];
     W->chunk_hash = C->chunk_hash;
     if (hipEventRecord(W->done, (hipStream_t)stream) != hipSuccess) throw Error(-FKS_EHIP, "window cache event");
+  }
+  if (Zc) {  // stored now (zmode 1) or read (zmode 2): stream-ordered like the windows
+    if (zmode == 1) {
+      Zc->valid = true;
+      Zc->seed = seeds[0];
+    }
+    if (hipEventRecord(Zc->done, (hipStream_t)stream) != hipSuccess) throw Error(-FKS_EHIP, "z-index cache event");
   }
 }
 

@@ -44,6 +44,12 @@
 #ifndef FKS_DB_MIN_WAVES
 #define FKS_DB_MIN_WAVES 4  // launch-bounds waves per SIMD of the double-buffered small-K kernel (6 WGs/CU measured 19 % slower than 5 at any bound)
 #endif
+#ifndef FKS_ZREPLAY_FLAT
+#define FKS_ZREPLAY_FLAT 1  // z-index replay: the flat streaming kernel (fks_zreplay_kernel), else small2 ZM 2
+#endif
+#ifndef FKS_ZREPLAY_DEPTH
+#define FKS_ZREPLAY_DEPTH 4  // z-index replay: blocks in flight per wave
+#endif
 #ifndef FKS_SM2_PF
 #define FKS_SM2_PF 1  // small-K kernel parameter prefetch distance in blocks (1 or 2)
 #endif
@@ -1195,6 +1201,14 @@ __device__ __forceinline__ u32x2_t temper_pair_u8x4(u32x2_t y) {
   return o;
 }
 
+// bf16 z pair from the two table byte offsets (x8) of temper_pair_u8x8: the lookups and
+// the rounding of z_pair_bf16_raw (default table layout)
+__device__ __forceinline__ f32x2_t z_bf16_idx8(uint32_t a8, uint32_t b8) {
+  const float r = lds_f32(a8 >> 1);
+  const f32x2_t rr = {r, r}, zero = {0.0f, 0.0f};
+  return rnd2<FKS_BF16>(__builtin_elementwise_fma(rr, lds_f32x2(kLdsCsOff + b8), zero));
+}
+
 template <int DT>
 __device__ __forceinline__ f32x2_t z_pair_sm2(const uint8_t* lds, uint32_t r1, uint32_t r2) {
   if constexpr (DT != FKS_BF16 || FKS_SM2_TAB == 0) {
@@ -1247,8 +1261,16 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
 }
 __device__ __forceinline__ float rflf(float v) { return __uint_as_float(rfl(__float_as_uint(v))); }
 
-template <int DT, int MODE>
+// z-index modes (bf16, one seed): ZM 1 = also store every block's table indices, one u32
+// per pair lane (bytes a_j, b_j, a_j+1, b_j+1: 1 B per parameter) at
+// zidx[(block - zlo) * 156 + q]; ZM 2 = REPLAY: no generator at all -- the indices come
+// from zidx (the ZO step's second and third calls, whose seed the first call used), so
+// no windows, no twist wave, no barriers: a streaming pass over p and the indices.
+constexpr int kZidxPerBlock = kSm2ZidxPerBlock;  // u32 per block
+static_assert(kSm2ZidxPerBlock == kSm2PairLanes, "one z-index word per pair lane");
+template <int DT, int MODE, int ZM = 0>
 __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_kernel(ApplyArgs a) {
+  static_assert(ZM == 0 || (DT == FKS_BF16 && FKS_SM2_TAB == 0 && !FKS_RPAIR), "z-index modes: bf16, default tables");
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
   if ((uint32_t)(size_t)(lds_u32_t*)lds32 != 0u) __builtin_trap();
@@ -1259,7 +1281,7 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
   const int nblk = (int)(a.chunk_block[c + 1] - b0);  // host: a chunk is far below 2^31 blocks
 
   if constexpr (DT == FKS_BF16) {
-    for (int i = tid; i < 256; i += kSm2Threads) {
+    for (int i = tid; i < 256; i += (int)blockDim.x) {  // (a replay launches 3 waves)
       if (FKS_SM2_TAB == 1) {
         reinterpret_cast<float*>(lds)[i] = c_tab_bf16[i];
         reinterpret_cast<float*>(lds + 1024)[i] = c_tab_bf16[256 + i];
@@ -1276,7 +1298,7 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
     }
   }
   // the chunk-start windows go to buffer 1, twisted into buffer 0 for block b0
-  for (int idx = tid; idx < nseeds * kMtN; idx += kSm2Threads) {
+  for (int idx = tid; ZM != 2 && idx < nseeds * kMtN; idx += kSm2Threads) {
     const int k = idx / kMtN, i = idx - k * kMtN;
     lds_st(kLdsTabBytes + (2 * k + 1) * kWinBytes + 4 * wperm(i), a.states[((size_t)k * a.nchunks + c) * kMtN + i]);
   }
@@ -1287,7 +1309,8 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
   // places wave w of every workgroup alike; vw is the wave's role index
   const int vw = FKS_SM2_ROT ? (plan.wave - (c & 3)) & 3 : plan.wave;
   __syncthreads();
-  if (vw == kSm2TwistWave) {
+  if (ZM == 2 && vw == kSm2TwistWave) return;  // (replay launches 3 waves; no twist)
+  if (ZM != 2 && vw == kSm2TwistWave) {
     auto twist_into = [&](auto dst_c) __attribute__((always_inline)) {
       constexpr int D = decltype(dst_c)::value;
 #pragma unroll
@@ -1308,7 +1331,7 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
     }
     return;
   }
-  __syncthreads();  // block b0 is in buffer 0
+  if (ZM != 2) __syncthreads();  // block b0 is in buffer 0
 
   const int vt = 64 * vw + (tid & 63);
   const int q = vt < kSm2PairLanes ? vt : kSm2PairLanes - 1;
@@ -1370,7 +1393,8 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
 
   // (cur at fetch time: the first segment ending after block t's start, where a
   // straddling block's lanes start their scan; fetching block t+1 may move cur on)
-  struct Slot { uint64_t base; int cur; bool fast; Pair r0, r1; };
+  struct Slot { uint64_t base; int cur; bool fast; Pair r0, r1; uint32_t zi; };
+  const uint32_t* zin = ZM == 2 ? a.zidx + ((size_t)(b0 - a.zlo)) * kZidxPerBlock + q : nullptr;
   auto fetch = [&](int t) __attribute__((always_inline)) -> Slot {
     Slot sl;
     while (t >= nb) { cur++; load_seg(); }
@@ -1386,23 +1410,40 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
       sl.r0 = 0;
       sl.r1 = 0;
     }
+    sl.zi = 0;
+    if constexpr (ZM == 2) sl.zi = zin[(size_t)(uint32_t)t * kZidxPerBlock];
     return sl;
   };
 
   // the block's four parameters through every seed of the pass, in seed order
-  auto run = [&](auto buf_c, Pair& r0, Pair& r1, float lr, float wd, bool wdf, float ps) __attribute__((always_inline)) {
+  // ZM 1: the block's seed-0 table offsets, computed once per block for every lane
+  u32x2_t zab = {0u, 0u}, zcd = {0u, 0u};
+  auto run = [&](auto buf_c, Pair& r0, Pair& r1, float lr, float wd, bool wdf, float ps, uint32_t zi) __attribute__((always_inline)) {
     constexpr int B = decltype(buf_c)::value;
     // pA = (p_j, p_j+8), pB = (p_j+1, p_j+9): the two Box-Muller pairs' parameters
     f32x2_t pA = {ST::cvt(ST::lo(r0)), ST::cvt(ST::lo(r1))};
     f32x2_t pB = {ST::cvt(ST::hi(r0)), ST::cvt(ST::hi(r1))};
+    if constexpr (ZM == 2) {
+      const f32x2_t zA = z_bf16_idx8((zi << 3) & 0x7F8u, (zi >> 5) & 0x7F8u);
+      const f32x2_t zB = z_bf16_idx8((zi >> 13) & 0x7F8u, (zi >> 21) & 0x7F8u);
+      pA = apply_pair<DT, MODE>(pA, zA, gk[0], lr, wd, wdf, ps, upd);
+      pB = apply_pair<DT, MODE>(pB, zB, gk[0], lr, wd, wdf, ps, upd);
+    } else {
 #pragma unroll
-    for (int k = 0; k < kSmallK; k++) {
-      if (k < nseeds) {  // wave-uniform
-        const u32x4_t w = lds_u4(st_off + (uint32_t)((2 * k + B) * kWinBytes));
-        const f32x2_t zA = z_pair_sm2<DT>(lds, w.x, w.y);
-        const f32x2_t zB = z_pair_sm2<DT>(lds, w.z, w.w);
-        pA = apply_pair<DT, MODE>(pA, zA, gk[k], lr, wd, wdf, ps, upd);
-        pB = apply_pair<DT, MODE>(pB, zB, gk[k], lr, wd, wdf, ps, upd);
+      for (int k = 0; k < kSmallK; k++) {
+        if (k < nseeds) {  // wave-uniform
+          f32x2_t zA, zB;
+          if (ZM == 1 && k == 0) {
+            zA = z_bf16_idx8(zab.x, zab.y);
+            zB = z_bf16_idx8(zcd.x, zcd.y);
+          } else {
+            const u32x4_t w = lds_u4(st_off + (uint32_t)((2 * k + B) * kWinBytes));
+            zA = z_pair_sm2<DT>(lds, w.x, w.y);
+            zB = z_pair_sm2<DT>(lds, w.z, w.w);
+          }
+          pA = apply_pair<DT, MODE>(pA, zA, gk[k], lr, wd, wdf, ps, upd);
+          pB = apply_pair<DT, MODE>(pB, zB, gk[k], lr, wd, wdf, ps, upd);
+        }
       }
     }
     if constexpr (sizeof(Pair) == 4) {  // bf16: the high halves of the bf16-exact results
@@ -1415,9 +1456,22 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
   };
 
   auto block = [&](auto buf_c, Slot& sl, int t) __attribute__((always_inline)) {
+    if constexpr (ZM == 1) {
+      constexpr int B = decltype(buf_c)::value;
+      const u32x4_t w = lds_u4(st_off + (uint32_t)(B * kWinBytes));
+      u32x2_t w0, w1;
+      w0.x = w.x;
+      w0.y = w.y;
+      w1.x = w.z;
+      w1.y = w.w;
+      zab = temper_pair_u8x8(w0);
+      zcd = temper_pair_u8x8(w1);
+      a.zidx[((size_t)(b0 + t - a.zlo)) * kZidxPerBlock + q] =
+          (zab.x >> 3) | (zab.y << 5) | (zcd.x << 13) | (zcd.y << 21);
+    }
     if (FKS_DIAG != 1) {
       if (sl.fast) {
-        run(buf_c, sl.r0, sl.r1, u_lr, u_wd, u_wdf, u_ps);
+        run(buf_c, sl.r0, sl.r1, u_lr, u_wd, u_wdf, u_ps, sl.zi);
         ST::store_pair(sl.base + joff, sl.r0);
         ST::store_pair(sl.base + joff + 8 * kEs, sl.r1);
       } else {
@@ -1438,15 +1492,33 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
             r0 = ST::load_pair(addr);
             r1 = ST::load_pair(addr + 8 * kEs);
           }
-          run(buf_c, r0, r1, sg.lr, sg.wd, (sg.flags & FKS_HAS_WD) != 0, sg.ps);
+          run(buf_c, r0, r1, sg.lr, sg.wd, (sg.flags & FKS_HAS_WD) != 0, sg.ps, sl.zi);
           ST::store_pair(addr, r0);
           ST::store_pair(addr + 8 * kEs, r1);
         }
       }
     }
-    __syncthreads();  // the twist wave has block t+1 in place
+    if (ZM != 2) __syncthreads();  // the twist wave has block t+1 in place
   };
 
+  if constexpr (ZM == 2) {
+    // replay: no barriers, so the wave streams; four blocks in flight per wave (the
+    // loads of a block are issued four blocks before its compute) to cover HBM latency
+    constexpr int kDepth = FKS_ZREPLAY_DEPTH;
+    Slot sr[kDepth];
+#pragma unroll
+    for (int u = 0; u < kDepth; u++) sr[u] = fetch(u < nblk ? u : 0);
+    for (int t = 0; t < nblk; t += kDepth) {
+#pragma unroll
+      for (int u = 0; u < kDepth; u++) {
+        if (t + u < nblk) {
+          block(std::integral_constant<int, 0>{}, sr[u], t + u);
+          if (t + u + kDepth < nblk) sr[u] = fetch(t + u + kDepth);
+        }
+      }
+    }
+    return;
+  }
 #if FKS_SM2_PF == 2
   // two blocks ahead: block t's slot is refilled with block t+2 right after its stores
   Slot s0 = fetch(0);
@@ -1471,6 +1543,127 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
     block(std::integral_constant<int, 1>{}, s1, t + 1);
   }
 #endif
+}
+
+// ------------------------------------------------------------------ z-index replay
+// fks_zreplay_kernel<MODE>: a one-seed bf16 pass whose z comes from the table indices a
+// fks_small2_kernel<.., ZM 1> pass stored for the same seed (ZCache): no generator, no
+// windows, no barriers -- a streaming pass.  Each thread takes 8 consecutive stream
+// positions (half a 16-block: 16 B of parameters, one dwordx4 load and store; a wave
+// covers 1 KB contiguously) and the 16-block's index record (16 B: a_i, b_i for its 8
+// Box-Muller pairs, at the record's stream offset: 1 byte per position), which both
+// halves of the 16-block read.  The first half takes z_i = R[a_i] C[b_i], the second
+// z_{i+8} = R[a_i] S[b_i] (DistributionTemplates.h:141-146), each rounded once as
+// z_pair_bf16_raw; then the update chain of apply_pair, element pairs (i, i+1).
+// Workgroup c walks the stream positions of chunk c in tiles of 256 x 8; a tile inside
+// one segment is addressed from a wave-uniform base, a straddling tile per lane.
+constexpr int kZrThreads = 256;
+typedef __attribute__((address_space(1))) u32x4_t gu32x4_t;
+__device__ __forceinline__ u32x4_t gload4(uint64_t addr) { return *reinterpret_cast<const gu32x4_t*>(addr); }
+__device__ __forceinline__ void gstore4(uint64_t addr, u32x4_t v) { *reinterpret_cast<gu32x4_t*>(addr) = v; }
+constexpr int kZrTile = kZrThreads * 8;  // stream positions per tile
+
+template <int MODE>
+__global__ __launch_bounds__(kZrThreads) void fks_zreplay_kernel(ApplyArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+  if ((uint32_t)(size_t)(lds_u32_t*)lds32 != 0u) __builtin_trap();
+  const int tid = threadIdx.x;
+  const int c = blockIdx.x;
+  // R | C | S as three f32[256]: one b32 lookup per table
+  for (int i = tid; i < 256; i += kZrThreads) {
+    reinterpret_cast<float*>(lds32)[i] = c_tab_bf16[i];
+    reinterpret_cast<float*>(lds32)[256 + i] = c_tab_bf16[256 + i];
+    reinterpret_cast<float*>(lds32)[512 + i] = c_tab_bf16[512 + i];
+  }
+  __syncthreads();
+  const int64_t p0 = (int64_t)kMtN * a.chunk_block[c], p1 = (int64_t)kMtN * a.chunk_block[c + 1];
+  const int64_t zbase = (int64_t)kMtN * a.zlo;
+  const uint64_t zb = (uint64_t)(uintptr_t)a.zidx;
+  float g = rflf(a.g[0]);
+  bool upd = true;
+  if (MODE == kModePerturbUpdate && a.gdev) {
+    g = dev_value_g<FKS_BF16>(a.gdev);
+    upd = dev_value_apply(a.gdev);
+  }
+  const uint32_t half = (uint32_t)tid & 1u;  // 0: first half of the 16-block (cos), 1: second (sin)
+  const uint32_t cs_tab = half ? 2048u : 1024u;
+
+  int cur = 0;
+  {
+    int lo = 0, hi = a.nsegs;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      const DevSeg& sm = a.segs[mid];
+      if ((int64_t)rfl64((uint64_t)(sm.start + sm.numel)) <= p0) lo = mid + 1; else hi = mid;
+    }
+    cur = lo;
+  }
+  // the 8 elements e[0..7] through the seed; z from the record's bytes
+  auto chain = [&](u32x4_t pv, u32x4_t rec, float lr, float wd, bool wdf, float ps) __attribute__((always_inline)) -> u32x4_t {
+    const uint32_t w[4] = {pv.x, pv.y, pv.z, pv.w};
+    const uint32_t r[4] = {rec.x, rec.y, rec.z, rec.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int m = 0; m < 4; m++) {  // elements 2m, 2m+1: pairs 2m (bytes 0,1 of r[m]) and 2m+1 (bytes 2,3)
+      const uint32_t ri = r[m];
+      const float ra = lds_f32((ri << 2) & 0x3FCu), rb = lds_f32((ri >> 14) & 0x3FCu);
+      const float ca = lds_f32(cs_tab + ((ri >> 6) & 0x3FCu)), cb = lds_f32(cs_tab + ((ri >> 22) & 0x3FCu));
+      const f32x2_t rr = {ra, rb}, cc = {ca, cb}, zero = {0.0f, 0.0f};
+      const f32x2_t z = rnd2<FKS_BF16>(__builtin_elementwise_fma(rr, cc, zero));
+      f32x2_t pe = {__uint_as_float(w[m] << 16), __uint_as_float(w[m] & 0xffff0000u)};
+      pe = apply_pair<FKS_BF16, MODE>(pe, z, g, lr, wd, wdf, ps, upd);
+      o[m] = __builtin_amdgcn_perm(__float_as_uint(pe.y), __float_as_uint(pe.x), 0x07060302u);
+    }
+    const u32x4_t out = {o[0], o[1], o[2], o[3]};
+    return out;
+  };
+  const u32x4_t zero4 = {0u, 0u, 0u, 0u};
+  for (int64_t t0 = p0; t0 < p1; t0 += kZrTile) {
+    const int64_t pos = t0 + 8 * (int64_t)tid;
+    // wave-uniform: the tile inside the current segment?
+    while (cur < a.nsegs) {
+      const int64_t en = (int64_t)rfl64((uint64_t)(a.segs[cur].start + a.segs[cur].numel));
+      if (en > t0) break;
+      cur++;
+    }
+    const int64_t tend = t0 + kZrTile < p1 ? t0 + kZrTile : p1;
+    bool fast = false;
+    uint64_t base = 0;
+    float lr = 0.0f, wd = 0.0f, ps = 0.0f;
+    bool wdf = false;
+    if (cur < a.nsegs) {
+      const DevSeg& sg = a.segs[cur];
+      const int64_t st = (int64_t)rfl64((uint64_t)sg.start);
+      const int64_t en = st + (int64_t)rfl64((uint64_t)sg.numel);
+      fast = st <= t0 && tend <= en;
+      base = rfl64(sg.ptr) + (uint64_t)(t0 - st) * 2u;
+      lr = rflf(sg.lr);
+      wd = rflf(sg.wd);
+      ps = rflf(sg.ps);
+      wdf = (rfl(sg.flags) & FKS_HAS_WD) != 0;
+    }
+    if (pos >= p1) continue;  // (the chunk's last tile; lanes past it idle)
+    const u32x4_t rec = gload4(zb + (uint64_t)((pos - zbase) & ~(int64_t)15));
+    if (fast) {
+      const uint64_t ptr = base + 16u * (uint32_t)tid;
+      const u32x4_t pv = MODE == kModeWriteZ ? zero4 : gload4(ptr);
+      gstore4(ptr, chain(pv, rec, lr, wd, wdf, ps));
+    } else {
+      int cc = cur;
+      bool in = false;
+      DevSeg sg;
+      while (cc < a.nsegs) {
+        sg = a.segs[cc];
+        if (pos < sg.start + sg.numel) { in = pos >= sg.start; break; }
+        cc++;
+      }
+      if (in) {
+        const uint64_t ptr = sg.ptr + (uint64_t)(pos - sg.start) * 2u;
+        const u32x4_t pv = MODE == kModeWriteZ ? zero4 : gload4(ptr);
+        gstore4(ptr, chain(pv, rec, sg.lr, sg.wd, (sg.flags & FKS_HAS_WD) != 0, sg.ps));
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------------ bf16 slice kernel
@@ -2141,21 +2334,36 @@ static int launch_apply_f(const ApplyArgs& a, void* stream) {
   return (int)hipGetLastError();
 }
 
-template <int DT, int MODE>
+template <int DT, int MODE, int ZM = 0>
 static int launch_small2(const ApplyArgs& a, void* stream) {
-  const size_t lds = (size_t)kLdsTabBytes + (size_t)(2 * a.nseeds + 1) * kWinBytes;
+  const size_t lds = ZM == 2 ? (size_t)kLdsTabBytes : (size_t)kLdsTabBytes + (size_t)(2 * a.nseeds + 1) * kWinBytes;
   static PerDevice attr;
   // the attribute is set once per device: for the largest pass this kernel takes
   constexpr int kMaxLds = kLdsTabBytes + (2 * kSmallK + 1) * kWinBytes;
-  if (int e = ensure_lds_attr(attr, &fks_small2_kernel<DT, MODE>, kMaxLds)) return e;
-  hipLaunchKernelGGL((fks_small2_kernel<DT, MODE>), dim3((unsigned)a.nchunks), dim3(kSm2Threads), lds,
-                     (hipStream_t)stream, a);
+  if (int e = ensure_lds_attr(attr, &fks_small2_kernel<DT, MODE, ZM>, kMaxLds)) return e;
+  hipLaunchKernelGGL((fks_small2_kernel<DT, MODE, ZM>), dim3((unsigned)a.nchunks),
+                     dim3(ZM == 2 ? kSm2Threads - 64 : kSm2Threads), lds, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 
 template <int DT, int MODE>
 static int launch_apply_t(const ApplyArgs& a, void* stream) {
   if (a.nseeds == kMaxSeedsPerPass) return launch_apply_f<DT, MODE, true>(a, stream);
+  if constexpr (DT == FKS_BF16 && FKS_SM2_TAB == 0 && !FKS_RPAIR) {
+    // one-seed bf16 passes with a z-index buffer (fks_capi.cpp ZCache): store / replay
+    if (a.zmode == 1 && a.nseeds == 1 && MODE == kModePerturb) return launch_small2<DT, MODE, 1>(a, stream);
+    if (a.zmode == 2 && a.nseeds == 1 &&
+        (MODE == kModePerturb || MODE == kModePerturbUpdate || MODE == kModeUpdate || MODE == kModeUpdateWd ||
+         MODE == kModeUpdateNoWd)) {
+      if (FKS_ZREPLAY_FLAT) {
+        hipLaunchKernelGGL((fks_zreplay_kernel<MODE>), dim3((unsigned)a.nchunks), dim3(kZrThreads),
+                           (size_t)3 * 1024, (hipStream_t)stream, a);
+        return (int)hipGetLastError();
+      }
+      return launch_small2<DT, MODE, 2>(a, stream);
+    }
+  }
+  if (a.zmode == 2) return -FKS_ENOTSUP;  // replay without a replay kernel: a host bug
   if (FKS_SMALL_V2 && a.nseeds <= kSmallK && DT != FKS_F16) return launch_small2<DT == FKS_F16 ? FKS_F32 : DT, MODE>(a, stream);
   if (FKS_SMALL_DBUF && a.nseeds <= kSmallK) return launch_apply_f<DT, MODE, false, true>(a, stream);
   return launch_apply_f<DT, MODE, false>(a, stream);

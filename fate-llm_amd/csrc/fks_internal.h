@@ -103,6 +103,9 @@ constexpr int kSmallK = 4;
 // v2: 56 VGPRs, 8 workgroups of 4 waves (8 waves/SIMD; K = 1, 2 fit 8 in LDS, K = 4 six):
 // perturb 7.2 ms at 8 WGs, 7.8 ms at 6 (profiles/r02_smallk_ab.log)
 constexpr int kSmallWgPerCu = FKS_SMALL_WG_PER_CU;
+// one-seed bf16 z indices (fks_small2_kernel ZM 1 / 2): one u32 per pair lane and block
+constexpr int kSm2ZidxPerBlock = 156;
+constexpr int kSm2ZidxBytesPerBlock = 4 * kSm2ZidxPerBlock;
 constexpr int kJumpThreads = 1024;  // 16 waves, one chunk's jump per wave at a time
 #ifndef FKS_JUMP_MAX_CPW
 #define FKS_JUMP_MAX_CPW 32  // most chunks one jump workgroup takes (fks_capi.cpp jump_chunks_per_wg)
@@ -130,6 +133,9 @@ struct ApplyArgs {
   const int64_t* chunk_block;   // [nchunks + 1] first MT block of each chunk
   uint64_t* sink;               // 4 KB of workspace: loads/stores of idle lanes (>= one block of f32 pairs)
   const float* gdev;            // kModePerturbUpdate from device memory: {g, apply} (nullptr: g[] above)
+  uint32_t* zidx;               // bf16 one-seed z indices: 156 u32 per block from block zlo (zmode 1 / 2)
+  int64_t zlo;
+  int32_t zmode;                // 0, 1 = store the indices while generating, 2 = replay them (no generator)
   int32_t nsegs;
   int32_t nchunks;
   int32_t nseeds;

@@ -128,7 +128,15 @@ int fks_profile_end(double* apply_ms, int64_t* n_apply, double* jump_ms, int64_t
  * jumped to in a library-owned per-device buffer, keyed by the seed and the chunk starts:
  * the zeroth-order step's three calls with one seed over one parameter list jump once.
  * Use across streams is ordered by an event (no host synchronisation); the buffer is
- * freed by fks_plan_cache_clear; FKS_NO_WIN_CACHE in the environment turns it off. */
+ * freed by fks_plan_cache_clear; FKS_NO_WIN_CACHE in the environment turns it off.
+ *
+ * One-seed bf16 perturbs also store the Box-Muller table indices of every MT block they
+ * cover (1 byte per parameter, a library-owned per-device buffer, allocated only while
+ * it stays a small share of the free device memory): a later one-seed perturb /
+ * perturb_step / K=1 update with the same seed over blocks inside that range replays
+ * the indices instead of running the generator -- the zeroth-order step's second and
+ * third calls, a streaming pass at 5 B of HBM traffic per parameter.  Values are
+ * identical either way; FKS_ZCACHE=0 turns it off; fks_plan_cache_clear frees it. */
 int fks_plan_cache_clear(void);
 
 /* torch.manual_seed(seed); for every tensor i in order: p = p + scales[i]*z, where

@@ -1,8 +1,10 @@
-"""The jumped-window cache of one-seed calls (fks_capi.cpp WinCache): a sequence of
-perturb / perturb_step / K=1 update calls that hits, misses (new seed, other tensor list
-with other chunk starts, shard), and moves to another stream and back (the buffer passes
-between streams through an event) gives the same parameters, bit for bit, as the same
-sequence with the cache off (FKS_NO_WIN_CACHE, read per call)."""
+"""The one-seed caches (fks_capi.cpp): the jumped-window cache (WinCache) and the bf16
+z-index cache (ZCache: a perturb stores every block's table indices, later calls with
+the same seed replay them without the generator).  A sequence of perturb / perturb_step
+/ K=1 update calls that hits, misses (new seed, other tensor list with other chunk
+starts, shard), and moves to another stream and back (the buffers pass between streams
+through events) gives the same parameters, bit for bit, with either cache or both on as
+with both off (FKS_NO_WIN_CACHE, FKS_ZCACHE=0, read per call)."""
 import os
 
 import pytest
@@ -34,24 +36,29 @@ def _sequence(params, side):
     torch.cuda.synchronize()
 
 
+CONFIGS = {"both": {}, "windows only": {"FKS_ZCACHE": "0"}, "z only": {"FKS_NO_WIN_CACHE": "1"},
+           "none": {"FKS_ZCACHE": "0", "FKS_NO_WIN_CACHE": "1"}}
+
+
 @pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
-def test_window_cache_matches_uncached(dtype):
+def test_caches_match_uncached(dtype):
+    from fate_llm.algo.fedkseed import _native as N
     dev = _dev()
-    shapes = [4096 * 3, 7, 1000, 624 * 5 + 3, 64]
+    shapes = [4096 * 3, 7, 1000, 624 * 5 + 3, 64, 624 * 40]
     arrays = rand_params(shapes, dtype, seed=71)
     side = torch.cuda.Stream(dev)
     out = {}
-    for cached in (True, False):
-        if cached:
-            os.environ.pop("FKS_NO_WIN_CACHE", None)
-        else:
-            os.environ["FKS_NO_WIN_CACHE"] = "1"
+    for name, env in CONFIGS.items():
+        N.check(N.load().fks_plan_cache_clear())  # every configuration starts with empty caches
+        os.environ.update(env)
         try:
             params = [from_np(a, dtype, dev) for a in arrays]
             _sequence(params, side)
-            out[cached] = [p.clone() for p in params]
+            out[name] = [p.clone() for p in params]
         finally:
-            os.environ.pop("FKS_NO_WIN_CACHE", None)
-    for i, (a, b) in enumerate(zip(out[True], out[False])):
-        assert torch.equal(a.view(torch.int16 if a.dtype == torch.bfloat16 else torch.int32),
-                           b.view(torch.int16 if b.dtype == torch.bfloat16 else torch.int32)), f"tensor {i}"
+            for key in env:
+                os.environ.pop(key, None)
+    view = torch.int16 if dtype == "bfloat16" else torch.int32
+    for name in ("both", "windows only", "z only"):
+        for i, (a, b) in enumerate(zip(out[name], out["none"])):
+            assert torch.equal(a.view(view), b.view(view)), f"{name}: tensor {i}"

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--params", type=int, default=0)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--ks", default="1,2,4,8,19")
+    ap.add_argument("--calls", default="", help="comma list: perturb,perturb_step,zo_step,replay (default all)")
     args = ap.parse_args()
     from fate_llm.algo.fedkseed import codec
 
@@ -65,10 +66,17 @@ def main():
         codec.perturb(views, sd(i), -1e-3)
         codec.perturb_step(specs, sd(i), [5e-4] * len(specs), 1.5)
 
-    measure("perturb", lambda i: codec.perturb(views, sd(i), 5e-4))
-    measure("perturb_step", lambda i: codec.perturb_step(specs, sd(i), [5e-4] * len(specs), 1.5))
-    measure("zo_step (3 calls)", zo_step)
-    for k in [int(x) for x in args.ks.split(",")]:
+    want = set(args.calls.split(",")) if args.calls else {"perturb", "perturb_step", "zo_step", "replay"}
+    if "perturb" in want:
+        measure("perturb", lambda i: codec.perturb(views, sd(i), 5e-4))
+    if "perturb_step" in want:
+        measure("perturb_step", lambda i: codec.perturb_step(specs, sd(i), [5e-4] * len(specs), 1.5))
+    if "zo_step" in want:
+        measure("zo_step (3 calls)", zo_step)
+    if "replay" in want:
+        # the same seed every time: after the first call, perturbs replay the stored z indices
+        measure("perturb, same seed (z-index replay)", lambda i: codec.perturb(views, sd(0), -1e-3))
+    for k in [int(x) for x in args.ks.split(",") if x]:
         measure(f"directional_step K={k}",
                 lambda i: codec.directional_step(specs, [sd(i + j) for j in range(k)], scalars[:k]))
 
