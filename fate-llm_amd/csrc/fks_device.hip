@@ -44,20 +44,8 @@
 #ifndef FKS_DB_MIN_WAVES
 #define FKS_DB_MIN_WAVES 4  // launch-bounds waves per SIMD of the double-buffered small-K kernel (6 WGs/CU measured 19 % slower than 5 at any bound)
 #endif
-#ifndef FKS_ZREPLAY_FLAT
-#define FKS_ZREPLAY_FLAT 1  // z-index replay: the flat streaming kernel (fks_zreplay_kernel), else small2 ZM 2
-#endif
-#ifndef FKS_ZREPLAY_DEPTH
-#define FKS_ZREPLAY_DEPTH 4  // z-index replay: blocks in flight per wave
-#endif
-#ifndef FKS_SM2_PF
-#define FKS_SM2_PF 1  // small-K kernel parameter prefetch distance in blocks (1 or 2)
-#endif
 #ifndef FKS_SM2_TWREG
 #define FKS_SM2_TWREG 1  // small-K twist wave: phases chained in registers (twist_oop_reg)
-#endif
-#ifndef FKS_SM2_ROT
-#define FKS_SM2_ROT 0  // small-K kernel: rotate the twist role across the workgroups' waves
 #endif
 #ifndef FKS_SM2_TAB
 #define FKS_SM2_TAB 0  // small-K kernel bf16 table layout: 0 R|(C,S) f32x2, 1 R|C|S f32, 2 R|(C,S) packed bf16
@@ -1261,16 +1249,17 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
 }
 __device__ __forceinline__ float rflf(float v) { return __uint_as_float(rfl(__float_as_uint(v))); }
 
-// z-index modes (bf16, one seed): ZM 1 = also store every block's table indices, one u32
-// per pair lane (bytes a_j, b_j, a_j+1, b_j+1: 1 B per parameter) at
-// zidx[(block - zlo) * 156 + q]; ZM 2 = REPLAY: no generator at all -- the indices come
-// from zidx (the ZO step's second and third calls, whose seed the first call used), so
-// no windows, no twist wave, no barriers: a streaming pass over p and the indices.
+// ZM 1 (bf16, one seed): also store every block's table indices, one u32 per pair lane
+// (bytes a_j, b_j, a_j+1, b_j+1: 1 B per parameter) at zidx[(block - zlo) * 156 + q],
+// for fks_zreplay_kernel to replay (the ZO step's second and third calls).  (A replay
+// through this kernel's own structure -- ZM 2, 3 waves, no twist -- streamed at 3.8
+// TB/s against 5.6 for the flat kernel: profiles/r02_smallk_ab.log.)
 constexpr int kZidxPerBlock = kSm2ZidxPerBlock;  // u32 per block
 static_assert(kSm2ZidxPerBlock == kSm2PairLanes, "one z-index word per pair lane");
 template <int DT, int MODE, int ZM = 0>
 __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_kernel(ApplyArgs a) {
-  static_assert(ZM == 0 || (DT == FKS_BF16 && FKS_SM2_TAB == 0 && !FKS_RPAIR), "z-index modes: bf16, default tables");
+  static_assert(ZM == 0 || (ZM == 1 && DT == FKS_BF16 && FKS_SM2_TAB == 0 && !FKS_RPAIR),
+                "z-index store: bf16, default tables");
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
   if ((uint32_t)(size_t)(lds_u32_t*)lds32 != 0u) __builtin_trap();
@@ -1298,19 +1287,17 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
     }
   }
   // the chunk-start windows go to buffer 1, twisted into buffer 0 for block b0
-  for (int idx = tid; ZM != 2 && idx < nseeds * kMtN; idx += kSm2Threads) {
+  for (int idx = tid; idx < nseeds * kMtN; idx += kSm2Threads) {
     const int k = idx / kMtN, i = idx - k * kMtN;
     lds_st(kLdsTabBytes + (2 * k + 1) * kWinBytes + 4 * wperm(i), a.states[((size_t)k * a.nchunks + c) * kMtN + i]);
   }
   TwistPlan plan;
   twist_plan(plan, tid, kLdsTabBytes);
-  // FKS_SM2_ROT: the twist role moves to wave (3 + c) % 4 of workgroup c, so the twist
-  // waves of the CU's workgroups do not all sit on the same SIMD when the dispatcher
-  // places wave w of every workgroup alike; vw is the wave's role index
-  const int vw = FKS_SM2_ROT ? (plan.wave - (c & 3)) & 3 : plan.wave;
+  // (rotating the twist role across the workgroups' waves, so that twist waves do not
+  // share a SIMD, measured no different: profiles/r02_smallk_ab.log)
+  const int vw = plan.wave;
   __syncthreads();
-  if (ZM == 2 && vw == kSm2TwistWave) return;  // (replay launches 3 waves; no twist)
-  if (ZM != 2 && vw == kSm2TwistWave) {
+  if (vw == kSm2TwistWave) {
     auto twist_into = [&](auto dst_c) __attribute__((always_inline)) {
       constexpr int D = decltype(dst_c)::value;
 #pragma unroll
@@ -1331,7 +1318,7 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
     }
     return;
   }
-  if (ZM != 2) __syncthreads();  // block b0 is in buffer 0
+  __syncthreads();  // block b0 is in buffer 0
 
   const int vt = 64 * vw + (tid & 63);
   const int q = vt < kSm2PairLanes ? vt : kSm2PairLanes - 1;
@@ -1393,8 +1380,7 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
 
   // (cur at fetch time: the first segment ending after block t's start, where a
   // straddling block's lanes start their scan; fetching block t+1 may move cur on)
-  struct Slot { uint64_t base; int cur; bool fast; Pair r0, r1; uint32_t zi; };
-  const uint32_t* zin = ZM == 2 ? a.zidx + ((size_t)(b0 - a.zlo)) * kZidxPerBlock + q : nullptr;
+  struct Slot { uint64_t base; int cur; bool fast; Pair r0, r1; };
   auto fetch = [&](int t) __attribute__((always_inline)) -> Slot {
     Slot sl;
     while (t >= nb) { cur++; load_seg(); }
@@ -1410,40 +1396,31 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
       sl.r0 = 0;
       sl.r1 = 0;
     }
-    sl.zi = 0;
-    if constexpr (ZM == 2) sl.zi = zin[(size_t)(uint32_t)t * kZidxPerBlock];
     return sl;
   };
 
   // the block's four parameters through every seed of the pass, in seed order
   // ZM 1: the block's seed-0 table offsets, computed once per block for every lane
   u32x2_t zab = {0u, 0u}, zcd = {0u, 0u};
-  auto run = [&](auto buf_c, Pair& r0, Pair& r1, float lr, float wd, bool wdf, float ps, uint32_t zi) __attribute__((always_inline)) {
+  auto run = [&](auto buf_c, Pair& r0, Pair& r1, float lr, float wd, bool wdf, float ps) __attribute__((always_inline)) {
     constexpr int B = decltype(buf_c)::value;
     // pA = (p_j, p_j+8), pB = (p_j+1, p_j+9): the two Box-Muller pairs' parameters
     f32x2_t pA = {ST::cvt(ST::lo(r0)), ST::cvt(ST::lo(r1))};
     f32x2_t pB = {ST::cvt(ST::hi(r0)), ST::cvt(ST::hi(r1))};
-    if constexpr (ZM == 2) {
-      const f32x2_t zA = z_bf16_idx8((zi << 3) & 0x7F8u, (zi >> 5) & 0x7F8u);
-      const f32x2_t zB = z_bf16_idx8((zi >> 13) & 0x7F8u, (zi >> 21) & 0x7F8u);
-      pA = apply_pair<DT, MODE>(pA, zA, gk[0], lr, wd, wdf, ps, upd);
-      pB = apply_pair<DT, MODE>(pB, zB, gk[0], lr, wd, wdf, ps, upd);
-    } else {
 #pragma unroll
-      for (int k = 0; k < kSmallK; k++) {
-        if (k < nseeds) {  // wave-uniform
-          f32x2_t zA, zB;
-          if (ZM == 1 && k == 0) {
-            zA = z_bf16_idx8(zab.x, zab.y);
-            zB = z_bf16_idx8(zcd.x, zcd.y);
-          } else {
-            const u32x4_t w = lds_u4(st_off + (uint32_t)((2 * k + B) * kWinBytes));
-            zA = z_pair_sm2<DT>(lds, w.x, w.y);
-            zB = z_pair_sm2<DT>(lds, w.z, w.w);
-          }
-          pA = apply_pair<DT, MODE>(pA, zA, gk[k], lr, wd, wdf, ps, upd);
-          pB = apply_pair<DT, MODE>(pB, zB, gk[k], lr, wd, wdf, ps, upd);
+    for (int k = 0; k < kSmallK; k++) {
+      if (k < nseeds) {  // wave-uniform
+        f32x2_t zA, zB;
+        if (ZM == 1 && k == 0) {
+          zA = z_bf16_idx8(zab.x, zab.y);
+          zB = z_bf16_idx8(zcd.x, zcd.y);
+        } else {
+          const u32x4_t w = lds_u4(st_off + (uint32_t)((2 * k + B) * kWinBytes));
+          zA = z_pair_sm2<DT>(lds, w.x, w.y);
+          zB = z_pair_sm2<DT>(lds, w.z, w.w);
         }
+        pA = apply_pair<DT, MODE>(pA, zA, gk[k], lr, wd, wdf, ps, upd);
+        pB = apply_pair<DT, MODE>(pB, zB, gk[k], lr, wd, wdf, ps, upd);
       }
     }
     if constexpr (sizeof(Pair) == 4) {  // bf16: the high halves of the bf16-exact results
@@ -1471,7 +1448,7 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
     }
     if (FKS_DIAG != 1) {
       if (sl.fast) {
-        run(buf_c, sl.r0, sl.r1, u_lr, u_wd, u_wdf, u_ps, sl.zi);
+        run(buf_c, sl.r0, sl.r1, u_lr, u_wd, u_wdf, u_ps);
         ST::store_pair(sl.base + joff, sl.r0);
         ST::store_pair(sl.base + joff + 8 * kEs, sl.r1);
       } else {
@@ -1492,45 +1469,16 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
             r0 = ST::load_pair(addr);
             r1 = ST::load_pair(addr + 8 * kEs);
           }
-          run(buf_c, r0, r1, sg.lr, sg.wd, (sg.flags & FKS_HAS_WD) != 0, sg.ps, sl.zi);
+          run(buf_c, r0, r1, sg.lr, sg.wd, (sg.flags & FKS_HAS_WD) != 0, sg.ps);
           ST::store_pair(addr, r0);
           ST::store_pair(addr + 8 * kEs, r1);
         }
       }
     }
-    if (ZM != 2) __syncthreads();  // the twist wave has block t+1 in place
+    __syncthreads();  // the twist wave has block t+1 in place
   };
 
-  if constexpr (ZM == 2) {
-    // replay: no barriers, so the wave streams; four blocks in flight per wave (the
-    // loads of a block are issued four blocks before its compute) to cover HBM latency
-    constexpr int kDepth = FKS_ZREPLAY_DEPTH;
-    Slot sr[kDepth];
-#pragma unroll
-    for (int u = 0; u < kDepth; u++) sr[u] = fetch(u < nblk ? u : 0);
-    for (int t = 0; t < nblk; t += kDepth) {
-#pragma unroll
-      for (int u = 0; u < kDepth; u++) {
-        if (t + u < nblk) {
-          block(std::integral_constant<int, 0>{}, sr[u], t + u);
-          if (t + u + kDepth < nblk) sr[u] = fetch(t + u + kDepth);
-        }
-      }
-    }
-    return;
-  }
-#if FKS_SM2_PF == 2
-  // two blocks ahead: block t's slot is refilled with block t+2 right after its stores
-  Slot s0 = fetch(0);
-  Slot s1 = fetch(nblk > 1 ? 1 : 0);
-  for (int t = 0; t < nblk; t += 2) {
-    block(std::integral_constant<int, 0>{}, s0, t);
-    if (t + 1 >= nblk) break;
-    if (t + 2 < nblk) s0 = fetch(t + 2);
-    block(std::integral_constant<int, 1>{}, s1, t + 1);
-    if (t + 3 < nblk) s1 = fetch(t + 3);
-  }
-#else
+  // (fetching two blocks ahead measured slower: profiles/r02_smallk_ab.log)
   Slot s0 = fetch(0);
   // a store after the first prefetch, so the loop is entered with the same pending
   // (load, store) shape as the back edge
@@ -1542,7 +1490,6 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
     s0 = fetch(t + 2 < nblk ? t + 2 : t + 1);
     block(std::integral_constant<int, 1>{}, s1, t + 1);
   }
-#endif
 }
 
 // ------------------------------------------------------------------ z-index replay
@@ -2336,13 +2283,13 @@ static int launch_apply_f(const ApplyArgs& a, void* stream) {
 
 template <int DT, int MODE, int ZM = 0>
 static int launch_small2(const ApplyArgs& a, void* stream) {
-  const size_t lds = ZM == 2 ? (size_t)kLdsTabBytes : (size_t)kLdsTabBytes + (size_t)(2 * a.nseeds + 1) * kWinBytes;
+  const size_t lds = (size_t)kLdsTabBytes + (size_t)(2 * a.nseeds + 1) * kWinBytes;
   static PerDevice attr;
   // the attribute is set once per device: for the largest pass this kernel takes
   constexpr int kMaxLds = kLdsTabBytes + (2 * kSmallK + 1) * kWinBytes;
   if (int e = ensure_lds_attr(attr, &fks_small2_kernel<DT, MODE, ZM>, kMaxLds)) return e;
-  hipLaunchKernelGGL((fks_small2_kernel<DT, MODE, ZM>), dim3((unsigned)a.nchunks),
-                     dim3(ZM == 2 ? kSm2Threads - 64 : kSm2Threads), lds, (hipStream_t)stream, a);
+  hipLaunchKernelGGL((fks_small2_kernel<DT, MODE, ZM>), dim3((unsigned)a.nchunks), dim3(kSm2Threads), lds,
+                     (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 
@@ -2355,12 +2302,9 @@ static int launch_apply_t(const ApplyArgs& a, void* stream) {
     if (a.zmode == 2 && a.nseeds == 1 &&
         (MODE == kModePerturb || MODE == kModePerturbUpdate || MODE == kModeUpdate || MODE == kModeUpdateWd ||
          MODE == kModeUpdateNoWd)) {
-      if (FKS_ZREPLAY_FLAT) {
-        hipLaunchKernelGGL((fks_zreplay_kernel<MODE>), dim3((unsigned)a.nchunks), dim3(kZrThreads),
-                           (size_t)3 * 1024, (hipStream_t)stream, a);
-        return (int)hipGetLastError();
-      }
-      return launch_small2<DT, MODE, 2>(a, stream);
+      hipLaunchKernelGGL((fks_zreplay_kernel<MODE>), dim3((unsigned)a.nchunks), dim3(kZrThreads), (size_t)3 * 1024,
+                         (hipStream_t)stream, a);
+      return (int)hipGetLastError();
     }
   }
   if (a.zmode == 2) return -FKS_ENOTSUP;  // replay without a replay kernel: a host bug
