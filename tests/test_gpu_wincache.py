@@ -62,3 +62,30 @@ def test_caches_match_uncached(dtype):
     for name in ("both", "windows only", "z only"):
         for i, (a, b) in enumerate(zip(out[name], out["none"])):
             assert torch.equal(a.view(view), b.view(view)), f"{name}: tensor {i}"
+
+
+def test_caches_match_uncached_mixed_dtypes():
+    """bf16 tensors next to f32 and f16 ones (and numel < 16 and ragged ones) in one list:
+    the bf16 fast segments replay their z indices while the f32 segments and the
+    irregular runs still generate from the (cached) windows of the same call."""
+    from fate_llm.algo.fedkseed import _native as N
+    dev = _dev()
+    layout = [("bfloat16", 4096 * 2), ("float32", 1024), ("bfloat16", 7), ("float16", 1000),
+              ("bfloat16", 624 * 9 + 5), ("float32", 33), ("bfloat16", 4096)]
+    arrays = [rand_params([n], dt, seed=91 + i)[0] for i, (dt, n) in enumerate(layout)]
+    side = torch.cuda.Stream(dev)
+    out = {}
+    for name, env in CONFIGS.items():
+        N.check(N.load().fks_plan_cache_clear())
+        os.environ.update(env)
+        try:
+            params = [from_np(a, dt, dev) for a, (dt, _) in zip(arrays, layout)]
+            _sequence(params, side)
+            out[name] = [p.clone() for p in params]
+        finally:
+            for key in env:
+                os.environ.pop(key, None)
+    for name in ("both", "windows only", "z only"):
+        for i, (a, b) in enumerate(zip(out[name], out["none"])):
+            w = torch.int32 if a.dtype == torch.float32 else torch.int16
+            assert torch.equal(a.view(w), b.view(w)), f"{name}: tensor {i} ({layout[i][0]})"
