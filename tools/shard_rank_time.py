@@ -1,0 +1,54 @@
+"""Per-rank work of the element-sharded reconstruct, measured on ONE GPU: rank 0's shard of
+the 7B bf16 K=4096 reconstruct for N = 1, 2, 4, 8 (the work each rank of an N-GPU run
+does; ranks share nothing on the data path).  Predicts the driver's strong-scaling
+efficiency t_1 / (N t_N) up to the max-over-ranks skew.
+python tools/shard_rank_time.py [--ns 1,2,4,8]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fate-llm_amd", "python"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ns", default="1,2,4,8")
+    args = ap.parse_args()
+    from fate_llm.algo.fedkseed import codec
+    dev = torch.device("cuda", 0)
+    shapes = bench.llama7b_shapes()
+    total = sum(bench.numel(s) for s in shapes)
+    flat = torch.empty(total, dtype=torch.bfloat16, device=dev).normal_(0.0, 0.02)
+    views, off = [], 0
+    for s in shapes:
+        views.append(flat[off:off + bench.numel(s)].view(s))
+        off += bench.numel(s)
+    specs = [codec.ParamSpec(v, lr=1e-5, weight_decay=0.01) for v in views]
+    seeds, vals = bench.synthetic_seeds(4096)
+    keep = [(s, v) for s, v in zip(seeds, vals) if v != 0.0]
+    ks, kv = [s for s, _ in keep], [v for _, v in keep]
+    t1 = None
+    for n in [int(x) for x in args.ns.split(",")]:
+        codec.directional_step(specs, ks[:40], kv[:40], shard=0, nshards=n)  # plan + warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with codec.profile() as prof:
+            codec.directional_step(specs, ks, kv, shard=0, nshards=n)
+            torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        t1 = t1 or dt * n
+        print(json.dumps({"nshards": n, "rank0_s": round(dt, 3), "apply_s": round(prof.apply_ms / 1e3, 3),
+                          "jump_s": round(prof.jump_ms / 1e3, 3),
+                          "predicted_efficiency": round(t1 / (n * dt), 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
