@@ -44,6 +44,12 @@
 #ifndef FKS_DB_MIN_WAVES
 #define FKS_DB_MIN_WAVES 4  // launch-bounds waves per SIMD of the double-buffered small-K kernel (6 WGs/CU measured 19 % slower than 5 at any bound)
 #endif
+#ifndef FKS_ZR_GRID
+#define FKS_ZR_GRID 1  // z-index replay: grid-stride tiles (1) or one chunk per workgroup (0)
+#endif
+#ifndef FKS_ZR_UNROLL
+#define FKS_ZR_UNROLL 2  // z-index replay: tiles per loop iteration (in flight per wave)
+#endif
 #ifndef FKS_SM2_TWREG
 #define FKS_SM2_TWREG 1  // small-K twist wave: phases chained in registers (twist_oop_reg)
 #endif
@@ -1523,7 +1529,13 @@ __global__ __launch_bounds__(kZrThreads) void fks_zreplay_kernel(ApplyArgs a) {
     reinterpret_cast<float*>(lds32)[512 + i] = c_tab_bf16[512 + i];
   }
   __syncthreads();
-  const int64_t p0 = (int64_t)kMtN * a.chunk_block[c], p1 = (int64_t)kMtN * a.chunk_block[c + 1];
+  // FKS_ZR_GRID: tiles of the whole call are dealt round-robin over the workgroups, so the
+  // workgroups in flight stream neighbouring addresses (few pages live at a time, as a
+  // grid-stride elementwise kernel); else workgroup c walks chunk c's tiles
+  const int64_t P0 = (int64_t)kMtN * a.chunk_block[0], P1 = (int64_t)kMtN * a.chunk_block[a.nchunks];
+  const int64_t p0 = FKS_ZR_GRID ? P0 + (int64_t)c * kZrTile : (int64_t)kMtN * a.chunk_block[c];
+  const int64_t p1 = FKS_ZR_GRID ? P1 : (int64_t)kMtN * a.chunk_block[c + 1];
+  const int64_t tstep = FKS_ZR_GRID ? (int64_t)gridDim.x * kZrTile : kZrTile;
   const int64_t zbase = (int64_t)kMtN * a.zlo;
   const uint64_t zb = (uint64_t)(uintptr_t)a.zidx;
   float g = rflf(a.g[0]);
@@ -1565,38 +1577,63 @@ __global__ __launch_bounds__(kZrThreads) void fks_zreplay_kernel(ApplyArgs a) {
     return out;
   };
   const u32x4_t zero4 = {0u, 0u, 0u, 0u};
-  for (int64_t t0 = p0; t0 < p1; t0 += kZrTile) {
-    const int64_t pos = t0 + 8 * (int64_t)tid;
-    // wave-uniform: the tile inside the current segment?
-    while (cur < a.nsegs) {
-      const int64_t en = (int64_t)rfl64((uint64_t)(a.segs[cur].start + a.segs[cur].numel));
-      if (en > t0) break;
-      cur++;
-    }
-    const int64_t tend = t0 + kZrTile < p1 ? t0 + kZrTile : p1;
-    bool fast = false;
-    uint64_t base = 0;
-    float lr = 0.0f, wd = 0.0f, ps = 0.0f;
-    bool wdf = false;
+  // FKS_ZR_UNROLL tiles per iteration: every tile's index records and parameters are
+  // loaded before the first is computed, so a wave keeps that many tiles in flight (a
+  // straddling tile loads its parameters when it runs)
+  struct ZSlot { int64_t t0; uint64_t base; float lr, wd, ps; int cur; bool fast, wdf; u32x4_t rec, pv; };
+  // the current segment's scalars, re-read only when the walk moves on (a global load
+  // here would wait for every load in flight, the prefetched tile's included)
+  int64_t seg_st = INT64_MAX, seg_en = INT64_MAX;
+  uint64_t seg_ptr = 0;
+  float seg_lr = 0.0f, seg_wd = 0.0f, seg_ps = 0.0f;
+  bool seg_wdf = false;
+  auto load_seg = [&]() __attribute__((always_inline)) {
     if (cur < a.nsegs) {
       const DevSeg& sg = a.segs[cur];
-      const int64_t st = (int64_t)rfl64((uint64_t)sg.start);
-      const int64_t en = st + (int64_t)rfl64((uint64_t)sg.numel);
-      fast = st <= t0 && tend <= en;
-      base = rfl64(sg.ptr) + (uint64_t)(t0 - st) * 2u;
-      lr = rflf(sg.lr);
-      wd = rflf(sg.wd);
-      ps = rflf(sg.ps);
-      wdf = (rfl(sg.flags) & FKS_HAS_WD) != 0;
-    }
-    if (pos >= p1) continue;  // (the chunk's last tile; lanes past it idle)
-    const u32x4_t rec = gload4(zb + (uint64_t)((pos - zbase) & ~(int64_t)15));
-    if (fast) {
-      const uint64_t ptr = base + 16u * (uint32_t)tid;
-      const u32x4_t pv = MODE == kModeWriteZ ? zero4 : gload4(ptr);
-      gstore4(ptr, chain(pv, rec, lr, wd, wdf, ps));
+      seg_st = (int64_t)rfl64((uint64_t)sg.start);
+      seg_en = seg_st + (int64_t)rfl64((uint64_t)sg.numel);
+      seg_ptr = rfl64(sg.ptr);
+      seg_lr = rflf(sg.lr);
+      seg_wd = rflf(sg.wd);
+      seg_ps = rflf(sg.ps);
+      seg_wdf = (rfl(sg.flags) & FKS_HAS_WD) != 0;
     } else {
-      int cc = cur;
+      seg_st = seg_en = INT64_MAX;
+    }
+  };
+  load_seg();
+  auto zfetch = [&](int64_t t0) __attribute__((always_inline)) -> ZSlot {
+    ZSlot z;
+    z.t0 = t0;
+    while (seg_en <= t0) {  // wave-uniform: the first segment ending after the tile's start
+      cur++;
+      load_seg();
+    }
+    z.cur = cur;
+    const int64_t tend = t0 + kZrTile < p1 ? t0 + kZrTile : p1;
+    z.fast = seg_st <= t0 && tend <= seg_en;
+    z.base = seg_ptr + (uint64_t)(t0 - seg_st) * 2u;
+    z.lr = seg_lr;
+    z.wd = seg_wd;
+    z.ps = seg_ps;
+    z.wdf = seg_wdf;
+    const int64_t pos = t0 + 8 * (int64_t)tid;
+    const bool live = pos < p1;  // (lanes past the chunk's end load lane 0's addresses)
+    z.rec = zero4;
+    z.pv = zero4;
+    if (t0 < p1) {  // wave-uniform
+      z.rec = gload4(zb + (uint64_t)(((live ? pos : t0) - zbase) & ~(int64_t)15));
+      if (MODE != kModeWriteZ && z.fast) z.pv = gload4(z.base + (live ? 16u * (uint32_t)tid : 0u));
+    }
+    return z;
+  };
+  auto zblock = [&](ZSlot& z) __attribute__((always_inline)) {
+    const int64_t pos = z.t0 + 8 * (int64_t)tid;
+    if (pos >= p1) return;
+    if (z.fast) {
+      gstore4(z.base + 16u * (uint32_t)tid, chain(z.pv, z.rec, z.lr, z.wd, z.wdf, z.ps));
+    } else {
+      int cc = z.cur;
       bool in = false;
       DevSeg sg;
       while (cc < a.nsegs) {
@@ -1607,9 +1644,17 @@ __global__ __launch_bounds__(kZrThreads) void fks_zreplay_kernel(ApplyArgs a) {
       if (in) {
         const uint64_t ptr = sg.ptr + (uint64_t)(pos - sg.start) * 2u;
         const u32x4_t pv = MODE == kModeWriteZ ? zero4 : gload4(ptr);
-        gstore4(ptr, chain(pv, rec, sg.lr, sg.wd, (sg.flags & FKS_HAS_WD) != 0, sg.ps));
+        gstore4(ptr, chain(pv, z.rec, sg.lr, sg.wd, (sg.flags & FKS_HAS_WD) != 0, sg.ps));
       }
     }
+  };
+  constexpr int kU = FKS_ZR_UNROLL;
+  for (int64_t t0 = p0; t0 < p1; t0 += kU * tstep) {
+    ZSlot z[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) z[u] = zfetch(t0 + u * tstep);
+#pragma unroll
+    for (int u = 0; u < kU; u++) zblock(z[u]);
   }
 }
 

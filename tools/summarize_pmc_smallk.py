@@ -9,7 +9,9 @@ import re
 import sys
 
 PARAMS = 6_738_415_616
-MODES = {"1": "perturb", "5": "perturb_update", "0": "update", "3": "update_wd", "4": "update_nowd"}
+MODES = {"1": "perturb", "5": "perturb_update", "0": "update", "3": "update_wd", "4": "update_nowd",
+         "1_store": "perturb_storing_z_indices", "replay_1": "perturb_replay", "replay_5": "perturb_update_replay",
+         "replay_3": "update_wd_replay", "replay_4": "update_nowd_replay", "replay_0": "update_replay"}
 
 
 def main(tag, variant):
@@ -18,10 +20,16 @@ def main(tag, variant):
         vals = collections.defaultdict(lambda: collections.defaultdict(float))
         dur = collections.defaultdict(dict)
         for r in csv.DictReader(open(f)):
-            m = re.search(r"(?:fks_apply_kernel<1, (\d+), false, true>|fks_small2_kernel<1, (\d+)>)", r["Kernel_Name"])
+            m = re.search(r"(fks_apply_kernel<1, (\d+), false, true>|fks_small2_kernel<1, (\d+)(?:, (\d))?>|"
+                          r"fks_zreplay_kernel<(\d+)>)", r["Kernel_Name"])
             if not m:
                 continue
-            mode = m.group(1) or m.group(2)
+            if m.group(5):
+                mode = "replay_" + m.group(5)
+            elif m.group(3):
+                mode = m.group(3) + ("_store" if m.group(4) == "1" else "")
+            else:
+                mode = m.group(2)
             vals[mode][(r["Counter_Name"], r["Dispatch_Id"])] += float(r["Counter_Value"])
             dur[mode][r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         for mode, d in vals.items():
