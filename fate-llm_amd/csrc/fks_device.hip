@@ -1631,7 +1631,11 @@ __global__ __launch_bounds__(kZrThreads) void fks_zreplay_kernel(ApplyArgs a) {
     const int64_t pos = z.t0 + 8 * (int64_t)tid;
     if (pos >= p1) return;
     if (z.fast) {
+#if FKS_DIAG == 8  // diagnostics: the replay's memory traffic without its arithmetic (wrong values)
+      gstore4(z.base + 16u * (uint32_t)tid, z.pv ^ z.rec);
+#else
       gstore4(z.base + 16u * (uint32_t)tid, chain(z.pv, z.rec, z.lr, z.wd, z.wdf, z.ps));
+#endif
     } else {
       int cc = z.cur;
       bool in = false;
