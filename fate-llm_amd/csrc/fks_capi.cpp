@@ -459,12 +459,14 @@ struct CachedPlan {
   bool have_bs = false;  // bf16 fast segments with their slice-kernel plan (non-small calls)
   uint64_t chunk_hash = 0;  // the chunk starts (regular + irregular): what a seed's windows depend on
   int64_t reg_lo = 0, reg_hi = 0;  // MT blocks [reg_lo, reg_hi) the regular chunks cover
+  uint64_t bf16_hash = 0;  // the bf16 segments' stream ranges: which blocks a z-index store covers
 };
 
 // Table indices of the last one-seed bf16 perturb, per device (ZO step: the second and
 // third calls replay them, fks_small2_kernel ZM 2).  A block's indices depend only on
 // the seed and the block's stream position, not on the tensors, so any later one-seed
-// call with the same seed whose regular blocks lie inside the stored range replays them.
+// call with the same seed and the same bf16 segment ranges (a store covers the blocks of
+// its own bf16 segments only) whose regular blocks lie inside the stored range replays them.
 // 1 byte per parameter of device memory; allocated only while it is a small share of the
 // free memory (FKS_ZCACHE=0 turns it off).  Stream hand-off by event, as WinCache.
 struct ZCache {
@@ -474,7 +476,7 @@ struct ZCache {
   void* stream = nullptr;
   hipEvent_t done = nullptr;
   bool valid = false;
-  uint64_t seed = 0;
+  uint64_t seed = 0, bf16_hash = 0;
   int64_t lo = 0, hi = 0;
 };
 
@@ -595,6 +597,12 @@ CachedPlan* build_plan(const fks_tensor* t, int nt, const double* scales, uint64
     key_put(ck, (int64_t)-1);
     for (int64_t b : IC.lo) key_put(ck, b);
     C->chunk_hash = fnv1a(ck);
+    std::vector<uint8_t> bk;
+    for (const DevSeg& sg : L.segs[FKS_BF16]) {
+      key_put(bk, sg.start);
+      key_put(bk, sg.numel);
+    }
+    C->bf16_hash = fnv1a(bk);
   }
   if (C->have_reg && !P.chunk_block.empty()) {
     C->reg_lo = P.chunk_block.front();
@@ -815,13 +823,15 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
   if (k == 1 && small && !use_bs && C->have_reg && C->nsegs[FKS_BF16] > 0 && z_mode_ok) {
     Zc = z_cache(stream, (size_t)kSm2ZidxBytesPerBlock * (size_t)(C->reg_hi - C->reg_lo));
     if (Zc) {
-      if (Zc->valid && Zc->seed == seeds[0] && Zc->lo <= C->reg_lo && C->reg_hi <= Zc->hi) {
+      if (Zc->valid && Zc->seed == seeds[0] && Zc->bf16_hash == C->bf16_hash && Zc->lo <= C->reg_lo &&
+          C->reg_hi <= Zc->hi) {
         zmode = 2;
       } else if (mode == kModePerturb) {
         zmode = 1;
         Zc->valid = false;  // until this call's store is launched
         Zc->lo = C->reg_lo;
         Zc->hi = C->reg_hi;
+        Zc->bf16_hash = C->bf16_hash;
       } else {
         Zc = nullptr;
       }
@@ -845,6 +855,19 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
       W->valid = false;  // until this call's jumps are launched
     }
   }
+  // a launch error still orders the cache buffers after this call's launches already
+  // queued (the entries stay invalid), so a next call on another stream cannot overtake them
+  struct EventsOnThrow {
+    WinCache*& W;
+    ZCache*& Z;
+    void* stream;
+    bool armed = true;
+    ~EventsOnThrow() {
+      if (!armed) return;
+      if (W) (void)hipEventRecord(W->done, (hipStream_t)stream);
+      if (Z) (void)hipEventRecord(Z->done, (hipStream_t)stream);
+    }
+  } on_throw{W, Zc, stream};
   auto gval = [&](int s, int d) -> float {
     return value_kind == FKS_VALUE_TENSOR ? round_to_dtype(values[s], d) : (float)values[s];
   };
@@ -938,6 +961,7 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
       check(timed(0, stream, [&] { return launch_irregular(ia, stream); }), "fks_irregular_kernel");
     }
   }
+  on_throw.armed = false;
   if (W) {  // this call's windows are in the cache (jumped now or reused), stream-ordered
     // (a replay that skipped the jump did not write the regular windows)
     W->valid = reg_cached || reg_jumped || !C->have_reg;

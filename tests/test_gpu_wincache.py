@@ -89,3 +89,32 @@ def test_caches_match_uncached_mixed_dtypes():
         for i, (a, b) in enumerate(zip(out[name], out["none"])):
             w = torch.int32 if a.dtype == torch.float32 else torch.int16
             assert torch.equal(a.view(w), b.view(w)), f"{name}: tensor {i} ({layout[i][0]})"
+
+
+def test_zcache_other_bf16_layout_same_range():
+    """Two tensor lists over the same stream range and seed whose bf16 segments cover
+    different blocks (bf16 then f32, and f32 then bf16): the second list's update must
+    not replay the first list's store, which holds no indices for its bf16 blocks."""
+    from fate_llm.algo.fedkseed import _native as N
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    n = 624 * 64
+    a_np = rand_params([n, n], "bfloat16", seed=5)
+    b_np = rand_params([n, n], "float32", seed=6)
+    out = {}
+    for name, env in (("both", {}), ("none", {"FKS_ZCACHE": "0", "FKS_NO_WIN_CACHE": "1"})):
+        N.check(N.load().fks_plan_cache_clear())
+        os.environ.update(env)
+        try:
+            first = [from_np(a_np[0], "bfloat16", dev), from_np(b_np[1], "float32", dev)]
+            second = [from_np(b_np[0], "float32", dev), from_np(a_np[1], "bfloat16", dev)]
+            codec.perturb(first, 21, 5e-4)                      # stores the first list's bf16 blocks
+            codec.directional_step([codec.ParamSpec(p, lr=1e-3) for p in second], [21], [0.75])
+            torch.cuda.synchronize()
+            out[name] = [p.clone() for p in first + second]
+        finally:
+            for key in env:
+                os.environ.pop(key, None)
+    for i, (a, b) in enumerate(zip(out["both"], out["none"])):
+        w = torch.int32 if a.dtype == torch.float32 else torch.int16
+        assert torch.equal(a.view(w), b.view(w)), f"tensor {i}"
