@@ -72,10 +72,20 @@
 #define FKS_BS_TAIL 0  // slice kernel: seeds of a block run after barrier 2, over the next rows' reads (0: measured best; 4/8/12 put the twist on the critical path: +9 / +15 / +25 %)
 #endif
 #ifndef FKS_BS_FENCE
-#define FKS_BS_FENCE 1  // slice kernel: compiler fence after every 8 seeds' table lookups
+#define FKS_BS_FENCE 8  // slice kernel: compiler fence after every FKS_BS_FENCE seeds' table lookups (0: none)
 #endif
 #ifndef FKS_BS_LA
-#define FKS_BS_LA 0  // slice kernel: table-lookup lookahead in seeds (0: compiler-scheduled; 4/6/8/12 measured 1.6/5.1/4.1/5.9 % slower, profiles/r02_slice_ab.log)
+#define FKS_BS_LA 0  // slice kernel: table-lookup lookahead in seeds (0: compiler-scheduled, each seed's reads waited with lgkmcnt(0); pinned pipelines of 1/2/3/4/6/8 seeds measured +6.7/+1.2/-0.3/+1.2/+2.9/+4.9 %, profiles/r02f_ab_la.log)
+#endif
+#ifndef FKS_BS_SCHED
+#define FKS_BS_SCHED 1  // slice kernel lookahead: scheduling barriers pin the software pipeline's order
+#endif
+#if FKS_BS_SCHED
+// the machine scheduler otherwise hoists a seed's z product right under its own table
+// reads (which then wait lgkmcnt(0) for the whole LDS latency)
+#define FKS_BS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define FKS_BS_SCHED_FENCE() asm volatile("" ::: "memory")
 #endif
 #ifndef FKS_BS_CSPACK
 #define FKS_BS_CSPACK 0  // slice kernel: (C,S) table as packed bf16 pairs (ds_read_b32) instead of f32 pairs (ds_read_b64)
@@ -1960,12 +1970,13 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
 #pragma unroll
         for (int k = 0; k < LA && k < kHead; k++)
           if (FULL || k < nseeds) lookup(k, lrr[k], lcs[k]);
-        asm volatile("" ::: "memory");
+        FKS_BS_SCHED_FENCE();
 #pragma unroll
         for (int k = 0; k < kHead; k++) {
           if (FULL || k < nseeds) p = chain(k, p, lrr[k % LA], lcs[k % LA]);
+          FKS_BS_SCHED_FENCE();
           if (k + LA < kHead && (FULL || k + LA < nseeds)) lookup(k + LA, lrr[k % LA], lcs[k % LA]);
-          asm volatile("" ::: "memory");
+          FKS_BS_SCHED_FENCE();
         }
       } else {
 #pragma unroll
@@ -1977,7 +1988,7 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
           }
           // the lookups of one byte column (8 seeds) at a time: hoisting all 64 table
           // reads ahead of the chain would spill
-          if (FKS_BS_FENCE && (k & 7) == 7) asm volatile("" ::: "memory");
+          if (FKS_BS_FENCE && (k % FKS_BS_FENCE) == FKS_BS_FENCE - 1) asm volatile("" ::: "memory");
         }
       }
     }
