@@ -79,3 +79,56 @@ def test_c2_full_size_chunking_seed_order_and_oracle_prefix():
     O.reconstruct(ref, [O.BF16], [1e-5], [0.01], ks, kv)
     got = whole[:PREFIX].view(torch.int16).cpu().numpy().view(np.uint16)
     assert_bitwise(got, ref[0], "bfloat16", "embedding prefix vs oracle")
+
+
+def test_zo_steps_full_size_caches_and_oracle_prefix():
+    """Three local zeroth-order steps (perturb +eps, perturb -2 eps, fused restore +
+    update; optimizer.py:108-150) over the full 7B bf16 layout: with the jumped-window
+    and z-index caches (the second and third pass of a step replay the first pass's
+    table indices) == with both caches off, bit for bit, and the embedding's first 4096
+    elements == the oracle's perturb / update sequence."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from fate_llm.algo.fedkseed import _native as N
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    shapes = bench.llama7b_shapes()
+    n = [bench.numel(s) for s in shapes]
+    base = torch.empty(sum(n), dtype=torch.bfloat16, device=dev)
+    base.normal_(0.0, 0.02, generator=torch.Generator(dev).manual_seed(3))
+    prefix = [base[:PREFIX].view(torch.int16).cpu().numpy().view(np.uint16).copy()]
+    eps, lr, wd = 5e-4, 1e-5, 0.01
+    steps = [(2718281828, -13.75), (97, 4.5), (4294967295, 0.0625)]
+
+    def run(buf):
+        views, off = [], 0
+        for s, m in zip(shapes, n):
+            views.append(buf[off:off + m].view(s))
+            off += m
+        specs = [codec.ParamSpec(v, lr=lr, weight_decay=wd) for v in views]
+        for seed, g in steps:
+            codec.perturb(views, seed, eps)
+            codec.perturb(views, seed, -2 * eps)
+            codec.perturb_step(specs, seed, [eps] * len(specs), g, value_is_tensor=False)
+        torch.cuda.synchronize()
+
+    out = {}
+    for name, env in (("cached", {}), ("uncached", {"FKS_ZCACHE": "0", "FKS_NO_WIN_CACHE": "1"})):
+        N.check(N.load().fks_plan_cache_clear())
+        os.environ.update(env)
+        try:
+            buf = base.clone()
+            run(buf)
+            out[name] = buf
+        finally:
+            for key in env:
+                os.environ.pop(key, None)
+    assert _differ(out["cached"], out["uncached"]) == 0, "z-index / window caches change the result"
+    del out["uncached"]
+    for seed, g in steps:
+        O.perturb_params(prefix, [O.BF16], seed, eps)
+        O.perturb_params(prefix, [O.BF16], seed, -2 * eps)
+        O.perturb_params(prefix, [O.BF16], seed, eps)
+        O.reconstruct(prefix, [O.BF16], [lr], [wd], [seed], [g])
+    got = out["cached"][:PREFIX].view(torch.int16).cpu().numpy().view(np.uint16)
+    assert_bitwise(got, prefix[0], "bfloat16", "embedding prefix vs oracle")
