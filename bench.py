@@ -237,10 +237,19 @@ def selftest(args, world, rank):
 
 # ------------------------------------------------------------------ GPU bench
 def run(args, world, rank, local):
+    # FKS_BENCH_SHARE_GPU=1 (rehearsal on a one-GPU box, tests/test_gpu_bench_ranks.py):
+    # the ranks share the visible GPUs and talk over gloo; the measured path is RCCL, one
+    # GPU per rank
+    share = os.environ.get("FKS_BENCH_SHARE_GPU") == "1"
+    if share:
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
         world = dist.get_world_size()  # what RCCL reports
 
     from fate_llm.algo.fedkseed import codec, zo_utils
@@ -351,6 +360,10 @@ def run(args, world, rank, local):
         "roofline_hbm": hbm,
         "jump_kernel_ms_per_step": round(prof.jump_ms / n_steps_prof, 2),
     }
+    if world > 1:
+        out["backend"] = dist.get_backend()
+        if share:
+            out["shared_gpu"] = True  # a rehearsal, not a measurement
     if gather_ms is not None:
         out["gather_ms"] = round(gather_ms, 1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
