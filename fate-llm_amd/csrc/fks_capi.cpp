@@ -584,9 +584,13 @@ CachedPlan* build_plan(const fks_tensor* t, int nt, const double* scales, uint64
     C->nsegs[d] = (int)L.segs[d].size();
     put(so, L.segs[d].data(), sizeof(DevSeg) * L.segs[d].size());
     so += sizeof(DevSeg) * L.segs[d].size();
-    size_t nwd = 0;
-    for (const DevSeg& sg : L.segs[d]) nwd += (sg.flags & FKS_HAS_WD) ? 1 : 0;
-    if (!L.segs[d].empty() && nwd == L.segs[d].size()) C->wd_mode[d] = kModeUpdateWd;
+    size_t nwd = 0, nwd0 = 0;
+    for (const DevSeg& sg : L.segs[d]) {
+      nwd += (sg.flags & FKS_HAS_WD) ? 1 : 0;
+      nwd0 += ((sg.flags & FKS_HAS_WD) && sg.wd == 0.0f) ? 1 : 0;  // +0.0 or -0.0
+    }
+    if (!L.segs[d].empty() && nwd0 == L.segs[d].size()) C->wd_mode[d] = kModeUpdateWd0;
+    else if (!L.segs[d].empty() && nwd == L.segs[d].size()) C->wd_mode[d] = kModeUpdateWd;
     else if (!L.segs[d].empty() && nwd == 0) C->wd_mode[d] = kModeUpdateNoWd;
   }
   put(C->H.off_runs, L.runs.data(), sizeof(DevRun) * L.runs.size());

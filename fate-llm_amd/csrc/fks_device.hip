@@ -888,11 +888,15 @@ __device__ __forceinline__ f32x2_t apply_pair(f32x2_t p, f32x2_t z, float g, flo
     p = rnd2<DT>(p + rnd2<DT>(ps * z));
     if (MODE == kModePerturb || !upd) return p;
   }
-  if (MODE == kModeUpdate || MODE == kModeUpdateWd || MODE == kModeUpdateNoWd || MODE == kModePerturbUpdate) {
+  if (MODE == kModeUpdate || MODE == kModeUpdateWd || MODE == kModeUpdateNoWd || MODE == kModePerturbUpdate ||
+      MODE == kModeUpdateWd0) {
     const f32x2_t gz = rnd2<DT>(g * z);
     f32x2_t t;
     if (MODE == kModeUpdateNoWd) {
       t = gz;
+    } else if (MODE == kModeUpdateWd0) {  // wd = +-0: rnd(gz + rnd(wd*p)) == fma(wd, p, gz) (fks_internal.h)
+      const f32x2_t ww = {wd, wd};
+      t = __builtin_elementwise_fma(ww, p, gz);
     } else {
       const f32x2_t t2 = rnd2<DT>(gz + rnd2<DT>(wd * p));
       if (MODE == kModeUpdateWd) {
@@ -2361,7 +2365,7 @@ static int launch_apply_t(const ApplyArgs& a, void* stream) {
     if (a.zmode == 1 && a.nseeds == 1 && MODE == kModePerturb) return launch_small2<DT, MODE, 1>(a, stream);
     if (a.zmode == 2 && a.nseeds == 1 &&
         (MODE == kModePerturb || MODE == kModePerturbUpdate || MODE == kModeUpdate || MODE == kModeUpdateWd ||
-         MODE == kModeUpdateNoWd)) {
+         MODE == kModeUpdateNoWd || MODE == kModeUpdateWd0)) {
       hipLaunchKernelGGL((fks_zreplay_kernel<MODE>), dim3((unsigned)a.nchunks), dim3(kZrThreads), (size_t)3 * 1024,
                          (hipStream_t)stream, a);
       return (int)hipGetLastError();
@@ -2383,6 +2387,7 @@ int launch_apply(int dtype, const ApplyArgs& a, void* stream) {
     case FKS_F32 * 8 + kModeUpdate: return launch_apply_t<FKS_F32, kModeUpdate>(a, stream);
     case FKS_F32 * 8 + kModeUpdateWd: return launch_apply_t<FKS_F32, kModeUpdateWd>(a, stream);
     case FKS_F32 * 8 + kModeUpdateNoWd: return launch_apply_t<FKS_F32, kModeUpdateNoWd>(a, stream);
+    case FKS_F32 * 8 + kModeUpdateWd0: return launch_apply_t<FKS_F32, kModeUpdateWd0>(a, stream);
     case FKS_F32 * 8 + kModePerturb: return launch_apply_t<FKS_F32, kModePerturb>(a, stream);
     case FKS_F32 * 8 + kModePerturbUpdate: return launch_apply_t<FKS_F32, kModePerturbUpdate>(a, stream);
     case FKS_F32 * 8 + kModeWriteZ: return launch_apply_t<FKS_F32, kModeWriteZ>(a, stream);
@@ -2390,6 +2395,7 @@ int launch_apply(int dtype, const ApplyArgs& a, void* stream) {
     case FKS_BF16 * 8 + kModeUpdate: return launch_apply_t<FKS_BF16, kModeUpdate>(a, stream);
     case FKS_BF16 * 8 + kModeUpdateWd: return launch_apply_t<FKS_BF16, kModeUpdateWd>(a, stream);
     case FKS_BF16 * 8 + kModeUpdateNoWd: return launch_apply_t<FKS_BF16, kModeUpdateNoWd>(a, stream);
+    case FKS_BF16 * 8 + kModeUpdateWd0: return launch_apply_t<FKS_BF16, kModeUpdateWd0>(a, stream);
     case FKS_BF16 * 8 + kModePerturb: return launch_apply_t<FKS_BF16, kModePerturb>(a, stream);
     case FKS_BF16 * 8 + kModePerturbUpdate: return launch_apply_t<FKS_BF16, kModePerturbUpdate>(a, stream);
     case FKS_BF16 * 8 + kModeWriteZ: return launch_apply_t<FKS_BF16, kModeWriteZ>(a, stream);
@@ -2421,6 +2427,7 @@ int launch_apply_bs(const ApplyBsArgs& a, void* stream) {
     case kModeUpdate: return launch_apply_bs_t<kModeUpdate>(a, stream);
     case kModeUpdateWd: return launch_apply_bs_t<kModeUpdateWd>(a, stream);
     case kModeUpdateNoWd: return launch_apply_bs_t<kModeUpdateNoWd>(a, stream);
+    case kModeUpdateWd0: return launch_apply_bs_t<kModeUpdateWd0>(a, stream);
     case kModeDelta: return launch_apply_bs_t<kModeDelta>(a, stream);
     default: return -FKS_ENOTSUP;
   }

@@ -114,13 +114,18 @@ constexpr int kJumpXLen = 19937 + 624;  // x[0..20560]: y[i + w] = x[i + w + 1],
 
 // kModeUpdateWd / kModeUpdateNoWd: kModeUpdate specialised for a launch whose segments
 // all have / all lack the weight-decay term (fast kernel only; chosen by the host)
+// kModeUpdateWd0: every segment has the term with wd = +-0.0 (the HF default the reference's
+// ClientTrainer passes, fedkseed.py:140): wd*p is exactly +-0 or NaN and gz + wd*p is
+// exactly gz, +-0 or NaN, so both roundings are identities and t = fma(wd, p, gz) gives
+// the same bits (signed zeros and NaNs included) with one instruction instead of six
+// per element pair
 // kModePerturbUpdate: p + ps*z, then the update with the same z (the restore
 // perturbation of zeroth_order_step fused with its directional step)
 // kModeDelta: the seed-sharded variant; z is accumulated into an f32 delta buffer,
 // delta += c_k * z (one fma), instead of updating the parameters
 enum ApplyMode : int {
   kModeUpdate = 0, kModePerturb = 1, kModeWriteZ = 2, kModeUpdateWd = 3, kModeUpdateNoWd = 4, kModePerturbUpdate = 5,
-  kModeDelta = 6
+  kModeDelta = 6, kModeUpdateWd0 = 7
 };
 
 // Per-pass seeds and multipliers travel BY VALUE in the kernel arguments: a call

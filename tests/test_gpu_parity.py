@@ -157,6 +157,37 @@ def test_edge_values(dtype):
 
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("wd", [0.0, -0.0])
+@pytest.mark.parametrize("k", [1, 3, 24, 40])
+def test_zero_weight_decay_edge_values(dtype, wd, k):
+    """weight_decay = +-0.0 (the HF default the reference's ClientTrainer passes) runs the
+    kModeUpdateWd0 chain, t = fma(wd, p, g*z) in place of rnd(g*z + rnd(wd*p)): it must keep
+    the reference's bits for zeros of both signs, infinities (inf*0 = NaN), NaNs and
+    denormals, with negative, tiny (g*z underflows to -0) and huge directional values.
+    K = 1, 3 take the small-K kernel, 24 / 40 the 19-seed fp32 or the 32-seed bf16 slice
+    kernel (one full pass and a partial one)."""
+    n = 64 * 1024
+    base = rand_params([n], dtype, seed=4)[0]
+    f = as_float(base, dtype).astype(np.float32)
+    f[:8] = [0.0, -0.0, np.inf, -np.inf, np.nan, 1e-40, -1e-39, 3e38]
+    f[8:16] = np.float32(-1.2e-38) * np.arange(8, dtype=np.float32)
+    f[5000:5016] = -0.0
+    f[7000:7016] = 0.0
+    arr = f if dtype == "float32" else to_np(torch.from_numpy(f).to(torch.bfloat16))
+    gg = torch.Generator().manual_seed(17 + k)
+    seeds = torch.randint(0, 2**32, (k,), generator=gg).tolist()
+    vals = (torch.randn(k, generator=gg, dtype=torch.float64) * 20).tolist()
+    edge = [-1e-45, 1e-45, -3e38, -5.0, 1e30, -0.5]
+    for i in range(1, min(k, len(edge) + 1)):  # seed 0 keeps an ordinary value
+        vals[i] = edge[i - 1]
+    got = _gpu_reconstruct([arr], dtype, [1e-2], [wd], seeds, vals)
+    O.reconstruct([arr], [DTC[dtype]], [1e-2], [wd], seeds, vals)
+    assert_bitwise(got[0], arr, dtype, f"wd {wd} k {k}")
+    # the specialised chain must have changed something besides the edge values
+    assert not np.array_equal(got[0][16:4096], base[16:4096])
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
 def test_tensor_valued_step_rounds_value_to_param_dtype(dtype):
     """zeroth_order_step passes g as a 0-dim fp32 tensor, the FIRST operand of g*z: torch
     casts it to the parameter dtype first (bf16 rounding)."""

@@ -1,7 +1,7 @@
 """A/B timing of apply-kernel builds: python tools/ab_apply.py [lib.so ...] (no argument:
 the in-tree libfks.so).  Each build runs in its own process (FKS_LIB_OVERRIDE) on the
 same workload -- N bf16 params (default 2^28), K seeds (default 95 = 5 full passes),
-wd on -- and prints the average apply/jump launch time per pass (AB_SEEDS seeds per
+wd AB_WD (default 0.01, 'none' for None) -- and prints the average apply/jump launch time per pass (AB_SEEDS seeds per
 launch for the per-seed figure: 19, or 32 for the bf16 slice kernel)."""
 import json
 import os
@@ -17,7 +17,8 @@ from fate_llm.algo.fedkseed import codec
 n, k = int(os.environ["AB_N"]), int(os.environ["AB_K"])
 dt = torch.float32 if os.environ.get("AB_DT") == "f32" else torch.bfloat16
 buf = torch.empty(n, dtype=dt, device="cuda").normal_(0, 0.02)
-specs = [codec.ParamSpec(buf, lr=1e-5, weight_decay=0.01)]
+wd = os.environ.get("AB_WD", "0.01")
+specs = [codec.ParamSpec(buf, lr=1e-5, weight_decay=None if wd == "none" else float(wd))]
 g = torch.Generator().manual_seed(1)
 seeds = torch.randint(0, 2**32, (k,), generator=g).tolist()
 vals = (torch.randn(k, generator=g, dtype=torch.float64) * 20).tolist()
@@ -28,7 +29,7 @@ for _ in range(3):
         codec.directional_step(specs, seeds, vals); torch.cuda.synchronize()
     r = p.apply_ms / max(p.n_apply, 1)
     best = r if best is None else min(best, r)
-print(json.dumps({"lib": os.environ.get("FKS_LIB_OVERRIDE", "libfks.so"), "dtype": str(dt), "n": n, "k": k,
+print(json.dumps({"lib": os.environ.get("FKS_LIB_OVERRIDE", "libfks.so"), "dtype": str(dt), "n": n, "k": k, "wd": wd,
                   "apply_ms_per_launch": round(best, 3),
                   "ps_per_seed_param": round(best * 1e9 / (n * int(os.environ.get("AB_SEEDS", "19"))), 3)}), flush=True)
 '''
