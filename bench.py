@@ -55,7 +55,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 VALU_PEAK_TLANEOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 VALU_MIX_CYCLES = 4.43
 VALU_MIX_CEILING_TLANEOPS = 1024 * 64 * 2.4e9 / VALU_MIX_CYCLES / 1e12
-PMC_SUMMARY = "pmc_apply_r02_full.json"  # the bf16 slice kernel (fks_apply_bs_kernel), tools/summarize_pmc2.py
+# per-launch counters of the bf16 slice kernel (fks_apply_bs_kernel), tools/summarize_pmc2.py: the
+# weight-decay chain (wd != 0) and the zero-weight-decay chain (kModeUpdateWd0)
+PMC_SUMMARIES = {"wd": "pmc_apply_r02_full.json", "wd0": "pmc_apply_r02g_wd0.json"}
 
 
 def llama7b_shapes():
@@ -87,11 +89,15 @@ def synthetic_seeds(k):
     return seeds, scalars
 
 
-def load_pmc_summary():
+def pmc_summary_name(wd):
+    return PMC_SUMMARIES["wd0" if wd == 0.0 else "wd"]
+
+
+def load_pmc_summary(wd):
     """Per-launch counters of the dominant kernel from the committed rocprofv3 --pmc
-    passes (profiles/PMC_SUMMARY, written by tools/summarize_pmc2.py)."""
+    passes (profiles/PMC_SUMMARIES, written by tools/summarize_pmc2.py)."""
     try:
-        with open(os.path.join(ROOT, "profiles", PMC_SUMMARY)) as f:
+        with open(os.path.join(ROOT, "profiles", pmc_summary_name(wd))) as f:
             return json.load(f)
     except OSError:
         return {}
@@ -105,6 +111,7 @@ torch.set_num_threads(1)
 from oracle import torch_replica as R
 from bench import synthetic_seeds
 n, first, step, budget = (int(os.environ[k]) for k in ("N", "FIRST", "STEP", "BUDGET"))
+wd = None if os.environ["WD"] == "none" else float(os.environ["WD"])
 s_, g_ = synthetic_seeds(4096)
 seeds = [(s, g) for s, g in zip(s_, g_) if g != 0.0]
 p = [torch.randn(n, generator=torch.Generator().manual_seed(0)).mul_(0.02).to(torch.bfloat16)]
@@ -113,13 +120,13 @@ for i in range(first, len(seeds), step):
     if time.perf_counter() - t0 > budget:
         break
     s, g = seeds[i]
-    R.reconstruct(p, [s], [g], 1e-5, 0.01)
+    R.reconstruct(p, [s], [g], 1e-5, wd)
     done += 1
 print(json.dumps({"done": done, "s": time.perf_counter() - t0}))
 '''
 
 
-def cpu_baseline(budget_s):
+def cpu_baseline(budget_s, wd):
     """The reference's CPU path (torch.manual_seed + torch.normal + the update expression
     of zo_utils.py:49, re-typed in oracle/torch_replica.py) on bounded samples of the
     same workload, scaled linearly to the 7B buffer x the 4055 non-zero seeds of K=4096:
@@ -139,7 +146,7 @@ def cpu_baseline(budget_s):
         done, t0 = 0, time.perf_counter()
         while done < len(keep) and time.perf_counter() - t0 < budget:
             s, g = keep[done]
-            R.reconstruct(p, [s], [g], 1e-5, 0.01)
+            R.reconstruct(p, [s], [g], 1e-5, wd)
             done += 1
         dt = time.perf_counter() - t0
         return dt / (n * done) * 1e9, done, dt
@@ -148,7 +155,7 @@ def cpu_baseline(budget_s):
     ns_big, d_big, dt_big = one_process(1 << 24, budget_s * 0.3)
     procs = max(1, min(16, os.cpu_count() or 1))
     n_all = 1 << 22
-    env = dict(os.environ, FKS_ROOT=ROOT, N=str(n_all), STEP=str(procs), BUDGET=str(int(max(2, budget_s * 0.5))),
+    env = dict(os.environ, FKS_ROOT=ROOT, N=str(n_all), WD="none" if wd is None else repr(wd), STEP=str(procs), BUDGET=str(int(max(2, budget_s * 0.5))),
                OMP_NUM_THREADS="1")
     kids = [subprocess.Popen([sys.executable, "-c", _CPU_CHILD], env=dict(env, FIRST=str(i)), stdout=subprocess.PIPE,
                              text=True) for i in range(procs)]
@@ -160,7 +167,8 @@ def cpu_baseline(budget_s):
     t7b_one = LLAMA7B_PARAMS * t7b_seeds * ns_big * 1e-9
     return {
         "value": LLAMA7B_PARAMS * 2 / t7b / 1e9, "unit": "GB/s", "cores": procs, "kind": "port",
-        "sample": (f"torch CPU replica of zo_utils.directional_derivative_step (oracle/torch_replica.py), "
+        "sample": (f"torch CPU replica of zo_utils.directional_derivative_step (oracle/torch_replica.py, "
+                   f"weight_decay {wd}), "
                    f"{procs} single-thread processes over disjoint seeds: {done_all} seeds x {n_all} bf16 params in "
                    f"{wall:.1f} s = {ns_all:.3f} ns per seed*param aggregate, scaled linearly to 6.74e9 params x "
                    f"{t7b_seeds} non-zero seeds ({t7b / 3600:.1f} h)"),
@@ -263,19 +271,20 @@ def run(args, world, rank, local):
     for s in shapes:
         views.append(flat[off:off + numel(s)].view(s))
         off += numel(s)
-    specs = [codec.ParamSpec(v, lr=1e-5, weight_decay=0.01) for v in views]
+    wd = args.wd
+    specs = [codec.ParamSpec(v, lr=1e-5, weight_decay=wd) for v in views]
     seeds, scalars = synthetic_seeds(args.k)
     keep = [(s, g) for s, g in zip(seeds, scalars) if g != 0.0]
     ks, kv = [s for s, _ in keep], [g for _, g in keep]
     seed_shard = args.mode == "seed-shard"
     if seed_shard:
-        groups = [{"params": views, "lr": 1e-5, "weight_decay": 0.01}]
+        groups = [{"params": views, "lr": 1e-5, "weight_decay": wd}]
         delta = torch.empty(total, dtype=torch.float32, device=dev)
     shard_words = [codec.shard_range(specs, r, world) for r in range(world)] if world > 1 else [(0, total)]
 
     def step():
         if seed_shard:
-            zo_utils.reconstruct_seed_sharded_(groups, ks, kv, lr=1e-5, weight_decay=0.01, delta=delta)
+            zo_utils.reconstruct_seed_sharded_(groups, ks, kv, lr=1e-5, weight_decay=wd, delta=delta)
         else:
             codec.directional_step(specs, ks, kv, shard=rank, nshards=world)
 
@@ -296,6 +305,19 @@ def run(args, world, rank, local):
         sync()
         gather_ms = max_over_ranks(time.perf_counter() - t0, world, dev) * 1e3
 
+    alt = None
+    if world == 1 and not seed_shard and args.alt_wd != wd:
+        # the same reconstruct at the other weight decay (plan built by a 32-seed call first)
+        alt_specs = [codec.ParamSpec(v, lr=1e-5, weight_decay=args.alt_wd) for v in views]
+        codec.directional_step(alt_specs, ks[:32], kv[:32])
+        sync()
+        t0 = time.perf_counter()
+        codec.directional_step(alt_specs, ks, kv)
+        sync()
+        alt_s = time.perf_counter() - t0
+        alt = {"weight_decay": args.alt_wd, "ms_per_step": round(alt_s * 1e3, 2),
+               "value": round(total * 2 / alt_s / 1e9, 4), "steps": 1}
+
     ms_per_step = dt / args.steps * 1e3
     buf_bytes = total * 2
     value = buf_bytes / (dt / args.steps) / 1e9
@@ -309,7 +331,7 @@ def run(args, world, rank, local):
     rank_seeds = len(ks) * (rank + 1) // world - len(ks) * rank // world if seed_shard else len(ks)
     seeds_per_launch = rank_seeds * n_steps_prof / n_apply
     units = rank_params * seeds_per_launch  # seed*param updates per launch
-    pmc = load_pmc_summary()
+    pmc = load_pmc_summary(wd)
     lane_ops = pmc.get("valu_lane_ops_per_seed_param")
     valu = None
     if lane_ops and not seed_shard:
@@ -325,7 +347,7 @@ def run(args, world, rank, local):
                 "counters": {k: pmc.get(k) for k in ("valu_active_frac", "valu_dual_issue_frac", "wait_any_frac",
                                                      "lds_bank_conflict_frac", "clock_ghz")},
                 "unit_def": ("one seed*param update (z draw + update chain); lane-ops = rocprofv3 SQ_INSTS_VALU x 64 "
-                             f"per seed*param (profiles/{PMC_SUMMARY}); peak = 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz "
+                             f"per seed*param (profiles/{pmc_summary_name(wd)}); peak = 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz "
                              "(MI355X_MICROARCH.md); mix_ceiling = the same chip issuing this kernel's "
                              f"single-issue instruction mix at the measured {VALU_MIX_CYCLES} cycles per "
                              "wave-instruction (profiles/r02_ubench_issue3.log)")}
@@ -355,6 +377,7 @@ def run(args, world, rank, local):
                    "1xMI355X: 7B-param bf16 buffer, K=4096 seeds" if world == 1 else
                    f"{world}xMI355X: 7B-param bf16 buffer, K=4096 seeds, element-sharded (bit-exact, no collective)",
                    "params": total, "k": args.k, "k_nonzero": len(ks), "tensors": len(shapes),
+                   "lr": 1e-5, "weight_decay": wd,
                    "parallelism": f"seed-shard{world}" if seed_shard else f"element-shard{world}"},
         "roofline": valu if valu else hbm,
         "roofline_hbm": hbm,
@@ -366,8 +389,10 @@ def run(args, world, rank, local):
             out["shared_gpu"] = True  # a rehearsal, not a measurement
     if gather_ms is not None:
         out["gather_ms"] = round(gather_ms, 1)
+    if alt is not None:
+        out["alt_weight_decay"] = alt
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_budget, wd)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -382,6 +407,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--k", type=int, default=4096)
     ap.add_argument("--params", type=int, default=0, help="override: flat buffer of this many params (dev only)")
+    ap.add_argument("--wd", type=lambda v: None if v == "none" else float(v), default=0.0,
+                    help="weight decay of every tensor (default 0.0: the HF TrainingArguments default the "
+                         "reference's ClientTrainer passes, fedkseed.py:140; 'none' = zo_utils.py:52)")
+    ap.add_argument("--alt-wd", type=lambda v: None if v == "none" else float(v), default=0.01,
+                    help="N = 1: one more timed reconstruct at this weight decay, reported beside value")
     ap.add_argument("--cpu-budget", type=float, default=24.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("sequential", "seed-shard"), default="sequential")

@@ -88,7 +88,10 @@
 #define FKS_BS_SCHED_FENCE() asm volatile("" ::: "memory")
 #endif
 #ifndef FKS_BS_CSPACK
-#define FKS_BS_CSPACK 0  // slice kernel: (C,S) table as packed bf16 pairs (ds_read_b32) instead of f32 pairs (ds_read_b64)
+// slice kernel: (C,S) table as packed bf16 pairs (ds_read_b32, two unpack ops) instead of f32 pairs
+// (ds_read_b64): 0 never, 1 always, 2 for the chains without the weight-decay roundings
+// (kModeUpdateWd0 / NoWd: 3.84 vs 4.03 ms per launch, profiles/r02g_ab_wd0.log)
+#define FKS_BS_CSPACK 2
 #endif
 #ifndef FKS_F32_RSQRT
 #define FKS_F32_RSQRT 0  // fp32 radius: 1 = v_sqrt_f32 + one residual step, no denormal scaling
@@ -1700,8 +1703,12 @@ constexpr int kBsStateBytes = 8 * kBsChunkBytes;       // 79,872
 // (C,S): f32 pairs (8 B, ds_read_b64) or, FKS_BS_CSPACK, the two bf16 values packed in one
 // dword (4 B, ds_read_b32): a random 8-bit-indexed ds_read_b64 measured 17.4 CU-cycles per
 // wave-instruction against 6.5 for ds_read_b32 (tools/ubench/issue2.hip), for two unpack ops
-constexpr int kBsCsBytes = FKS_BS_CSPACK ? 4 : 8;
-constexpr int kBsTabBytes = 256 * 4 + 256 * kBsCsBytes;  // 2,048 (3,072)
+constexpr int kBsCsBytes = 8;                          // room for either layout
+constexpr int kBsTabBytes = 256 * 4 + 256 * kBsCsBytes;  // 3,072
+template <int MODE>
+constexpr bool bs_cspack() {
+  return FKS_BS_CSPACK == 1 || (FKS_BS_CSPACK == 2 && (MODE == kModeUpdateWd0 || MODE == kModeUpdateNoWd));
+}
 constexpr int kBsLdsBytes = kBsTabBytes + 2 * kBsStateBytes;  // 162,816 <= 163,840
 static_assert(kBsLdsBytes <= 163840, "slice kernel LDS");
 
@@ -1804,7 +1811,7 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
 
   for (int i = tid; i < 256; i += kBsThreads) {
     reinterpret_cast<float*>((uint8_t*)lds32)[i] = c_tab_bf16[i];
-    if (FKS_BS_CSPACK)  // C in the low half, S in the high half (both exact bf16 values)
+    if (bs_cspack<MODE>())  // C in the low half, S in the high half (both exact bf16 values)
       reinterpret_cast<uint32_t*>((uint8_t*)lds32 + 1024)[i] =
           (__float_as_uint(c_tab_bf16[256 + i]) >> 16) | (__float_as_uint(c_tab_bf16[512 + i]) & 0xffff0000u);
     else
@@ -1918,14 +1925,14 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   // seed k's table lookups (R[a], (C,S)[b]) and its step of the update chain
   auto lookup = [&](int k, f32x2_t& rr, f32x2_t& cs) {
     const uint32_t ia = bs_index<2>(oa[k & 7], k >> 3);
-    const uint32_t ib = bs_index<FKS_BS_CSPACK ? 2 : 3>(ob[k & 7], k >> 3);
+    const uint32_t ib = bs_index<bs_cspack<MODE>() ? 2 : 3>(ob[k & 7], k >> 3);
 #if FKS_BS_DIAG == 3  // diagnostics: no table lookups (wrong values)
     rr = f32x2_t{__uint_as_float(ia | 0x3f800000u), __uint_as_float(ia | 0x3f800000u)};
     cs = f32x2_t{__uint_as_float(ib | 0x3f000000u), __uint_as_float(ib | 0x3e000000u)};
 #else
     const float r = lds_f32(ia);
     rr = f32x2_t{r, r};
-    if (FKS_BS_CSPACK) {
+    if (bs_cspack<MODE>()) {
       const uint32_t w = lds_u32((int)(1024u + ib));
       cs = f32x2_t{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
     } else {

@@ -44,7 +44,7 @@ def test_cpu_baseline_leg_runs():
     sys.path.insert(0, ROOT)
     import bench
 
-    cb = bench.cpu_baseline(3.0)
+    cb = bench.cpu_baseline(3.0, 0.0)
     assert cb["kind"] == "port" and cb["unit"] == "GB/s" and cb["value"] > 0
     assert 1 <= cb["cores"] <= 16
     sp = cb["single_process"]

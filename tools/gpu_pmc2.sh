@@ -9,7 +9,10 @@ GROUPS_=("SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTI
          "FETCH_SIZE GRBM_GUI_ACTIVE"
          "WRITE_SIZE GRBM_GUI_ACTIVE")
 for v in ${VARIANTS:-full}; do
-  if [ "$v" != "full" ]; then export FKS_LIB_OVERRIDE=$PWD/fate-llm_amd/build/libfks_$v.so; else unset FKS_LIB_OVERRIDE; fi
+  # full: the in-tree library at wd 0.01; wd0: the in-tree library at wd 0.0 (kModeUpdateWd0)
+  if [ "$v" = "wd0" ]; then unset FKS_LIB_OVERRIDE; export PERF_WD=0.0
+  elif [ "$v" != "full" ]; then export FKS_LIB_OVERRIDE=$PWD/fate-llm_amd/build/libfks_$v.so; unset PERF_WD
+  else unset FKS_LIB_OVERRIDE; unset PERF_WD; fi
   i=0
   for g in "${GROUPS_[@]}"; do
     rm -rf gpurun_out/pmc2_${v}_$i
