@@ -87,6 +87,9 @@
 #else
 #define FKS_BS_SCHED_FENCE() asm volatile("" ::: "memory")
 #endif
+#ifndef FKS_BS_ROLEMAP
+#define FKS_BS_ROLEMAP 0  // slice kernel: wave roles (0: twist waves 5 and 11, on SIMDs 1 and 3; 1: 5 and 9, both on SIMD 1 beside one pair wave: +5 %, profiles/r02i_ab.log)
+#endif
 #ifndef FKS_BS_CSPACK
 // slice kernel: (C,S) table as packed bf16 pairs (ds_read_b32, two unpack ops) instead of f32 pairs
 // (ds_read_b64): 0 never, 1 always, 2 for the chains without the weight-decay roundings
@@ -1795,10 +1798,19 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   if ((uint32_t)(size_t)(lds_u32_t*)lds32 != 0u) __builtin_trap();
   const int tid = threadIdx.x;
+  const int lane = tid & 63;
+#if FKS_BS_ROLEMAP == 1
+  // waves w, w+4, w+8 share a SIMD (profiles/r02f_simdmap.log): the two twist waves at
+  // w = 5 (half 0) and w = 9 (half 1) share SIMD 1 with one pair wave
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int half = w >= 6 ? 1 : 0;
+  const int hw = w < 5 ? w : (w == 5 || w == 9 ? 5 : (w < 9 ? w - 6 : w - 7));
+  const int ht = hw * 64 + lane;
+#else
   const int half = __builtin_amdgcn_readfirstlane(tid >= kBsHalfThreads ? 1 : 0);
   const int ht = tid - half * kBsHalfThreads;
   const int hw = __builtin_amdgcn_readfirstlane(ht >> 6);  // 0..4 pair waves, 5 twist wave
-  const int lane = tid & 63;
+#endif
   const int c = kBsChunksPerWg * (int)blockIdx.x + half;
   const int nseeds = FULL ? kBsSeeds : a.nseeds;
   const int64_t b0 = a.chunk_block[c], b1 = a.chunk_block[c + 1];
