@@ -90,6 +90,9 @@
 #ifndef FKS_BS_ROLEMAP
 #define FKS_BS_ROLEMAP 0  // slice kernel: wave roles (0: twist waves 5 and 11, on SIMDs 1 and 3; 1: 5 and 9, both on SIMD 1 beside one pair wave: +5 %, profiles/r02i_ab.log)
 #endif
+#ifndef FKS_BS_PLANAR
+#define FKS_BS_PLANAR 0  // slice kernel: C and S as two f32 tables 1 KB apart, one ds_read2st64_b32 per seed (measured +19 % at wd 0.0, +8 % at wd 0.01: profiles/r02j_ab_planar.log)
+#endif
 #ifndef FKS_BS_CSPACK
 // slice kernel: (C,S) table as packed bf16 pairs (ds_read_b32, two unpack ops) instead of f32 pairs
 // (ds_read_b64): 0 never, 1 always, 2 for the chains without the weight-decay roundings
@@ -1710,7 +1713,8 @@ constexpr int kBsCsBytes = 8;                          // room for either layout
 constexpr int kBsTabBytes = 256 * 4 + 256 * kBsCsBytes;  // 3,072
 template <int MODE>
 constexpr bool bs_cspack() {
-  return FKS_BS_CSPACK == 1 || (FKS_BS_CSPACK == 2 && (MODE == kModeUpdateWd0 || MODE == kModeUpdateNoWd));
+  return !FKS_BS_PLANAR &&
+         (FKS_BS_CSPACK == 1 || (FKS_BS_CSPACK == 2 && (MODE == kModeUpdateWd0 || MODE == kModeUpdateNoWd)));
 }
 constexpr int kBsLdsBytes = kBsTabBytes + 2 * kBsStateBytes;  // 162,816 <= 163,840
 static_assert(kBsLdsBytes <= 163840, "slice kernel LDS");
@@ -1823,7 +1827,10 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
 
   for (int i = tid; i < 256; i += kBsThreads) {
     reinterpret_cast<float*>((uint8_t*)lds32)[i] = c_tab_bf16[i];
-    if (bs_cspack<MODE>())  // C in the low half, S in the high half (both exact bf16 values)
+    if (FKS_BS_PLANAR) {
+      reinterpret_cast<float*>((uint8_t*)lds32 + 1024)[i] = c_tab_bf16[256 + i];
+      reinterpret_cast<float*>((uint8_t*)lds32 + 2048)[i] = c_tab_bf16[512 + i];
+    } else if (bs_cspack<MODE>())  // C in the low half, S in the high half (both exact bf16 values)
       reinterpret_cast<uint32_t*>((uint8_t*)lds32 + 1024)[i] =
           (__float_as_uint(c_tab_bf16[256 + i]) >> 16) | (__float_as_uint(c_tab_bf16[512 + i]) & 0xffff0000u);
     else
@@ -1937,14 +1944,16 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   // seed k's table lookups (R[a], (C,S)[b]) and its step of the update chain
   auto lookup = [&](int k, f32x2_t& rr, f32x2_t& cs) {
     const uint32_t ia = bs_index<2>(oa[k & 7], k >> 3);
-    const uint32_t ib = bs_index<bs_cspack<MODE>() ? 2 : 3>(ob[k & 7], k >> 3);
+    const uint32_t ib = bs_index<(bs_cspack<MODE>() || FKS_BS_PLANAR) ? 2 : 3>(ob[k & 7], k >> 3);
 #if FKS_BS_DIAG == 3  // diagnostics: no table lookups (wrong values)
     rr = f32x2_t{__uint_as_float(ia | 0x3f800000u), __uint_as_float(ia | 0x3f800000u)};
     cs = f32x2_t{__uint_as_float(ib | 0x3f000000u), __uint_as_float(ib | 0x3e000000u)};
 #else
     const float r = lds_f32(ia);
     rr = f32x2_t{r, r};
-    if (bs_cspack<MODE>()) {
+    if (FKS_BS_PLANAR) {  // C[b] and S[b] 1024 B apart: one ds_read2st64_b32
+      cs = f32x2_t{lds_f32(1024u + ib), lds_f32(2048u + ib)};
+    } else if (bs_cspack<MODE>()) {
       const uint32_t w = lds_u32((int)(1024u + ib));
       cs = f32x2_t{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
     } else {
