@@ -39,7 +39,7 @@
 #endif
 #ifndef FKS_BS_DIAG
 #define FKS_BS_DIAG 0  // slice kernel diagnostics (wrong results): 1 no twist, 2 no pair chain, 3 no lookups,
-                        // 5 no barriers in the block loop
+                        // 5 no barriers in the block loop, 6 twist without stores, 7 twist without loads
 #endif
 #ifndef FKS_DB_MIN_WAVES
 #define FKS_DB_MIN_WAVES 4  // launch-bounds waves per SIMD of the double-buffered small-K kernel (6 WGs/CU measured 19 % slower than 5 at any bound)
@@ -1769,13 +1769,25 @@ __device__ __forceinline__ void bs_twist_block(uint32_t sbase, int lane) {
     if (r + 1 < 10) {
       uint32_t avn, amn;
       bs_round_rows(sbase, r + 1, lane, avn, amn);
+#if FKS_BS_DIAG == 7  // diagnostics: the twist loads nothing after round 0 (wrong values)
+#pragma unroll
+      for (int b = 0; b < 32; b++) {
+        Vn[b] = V[b] ^ avn;
+        Mn[b] = M[b] ^ amn;
+      }
+#else
       bs_load_row(avn, Vn);
       bs_load_row(amn, Mn);
+#endif
     }
     const uint32_t u31 = (uint32_t)__builtin_amdgcn_update_dpp((int)prev63, (int)V[31], 0x138, 0xF, 0xF, false);
     prev63 = (uint32_t)__builtin_amdgcn_readlane((int)V[31], 63);
     bs::twist_row_inplace(V, M, u31);  // M now holds the new row i
+#if FKS_BS_DIAG == 6  // diagnostics: the twist stores nothing (wrong values)
+    if (r == 9 && 64 * r + lane < 0) bs_store_row(sbase + 16u * (uint32_t)(64 * r + lane), M);
+#else
     if (r < 9 || 64 * r + lane < kMtN) bs_store_row(sbase + 16u * (uint32_t)(64 * r + lane), M);
+#endif
     if (r + 1 < 10) {
 #pragma unroll
       for (int b = 0; b < 32; b++) {
