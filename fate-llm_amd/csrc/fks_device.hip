@@ -87,6 +87,9 @@
 #else
 #define FKS_BS_SCHED_FENCE() asm volatile("" ::: "memory")
 #endif
+#ifndef FKS_WD0_F32
+#define FKS_WD0_F32 1  // the zero-weight-decay fma form also in the fp32 kernels (0: the full chain there)
+#endif
 #ifndef FKS_BS_ROLEMAP
 #define FKS_BS_ROLEMAP 0  // slice kernel: wave roles (0: twist waves 5 and 11, on SIMDs 1 and 3; 1: 5 and 9, both on SIMD 1 beside one pair wave: +5 %, profiles/r02i_ab.log)
 #endif
@@ -903,7 +906,8 @@ __device__ __forceinline__ f32x2_t apply_pair(f32x2_t p, f32x2_t z, float g, flo
     f32x2_t t;
     if (MODE == kModeUpdateNoWd) {
       t = gz;
-    } else if (MODE == kModeUpdateWd0) {  // wd = +-0: rnd(gz + rnd(wd*p)) == fma(wd, p, gz) (fks_internal.h)
+    } else if (MODE == kModeUpdateWd0 && (DT != FKS_F32 || FKS_WD0_F32)) {
+      // wd = +-0: rnd(gz + rnd(wd*p)) == fma(wd, p, gz) (fks_internal.h)
       const f32x2_t ww = {wd, wd};
       t = __builtin_elementwise_fma(ww, p, gz);
     } else {
