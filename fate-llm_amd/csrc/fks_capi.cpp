@@ -518,6 +518,9 @@ void key_put(std::vector<uint8_t>& k, const T& v) {
   k.insert(k.end(), p, p + sizeof(T));
 }
 
+#ifndef FKS_WD0_F32_MODE
+#define FKS_WD0_F32_MODE 1  // fp32 launches with wd = +-0 take kModeUpdateWd0 (0: kModeUpdateWd, the same bits)
+#endif
 std::vector<uint8_t> plan_key(const fks_tensor* t, int nt, const double* scales, uint64_t delta_base, int shard,
                               int nshards, bool small) {
   std::vector<uint8_t> k;
@@ -589,7 +592,8 @@ CachedPlan* build_plan(const fks_tensor* t, int nt, const double* scales, uint64
       nwd += (sg.flags & FKS_HAS_WD) ? 1 : 0;
       nwd0 += ((sg.flags & FKS_HAS_WD) && sg.wd == 0.0f) ? 1 : 0;  // +0.0 or -0.0
     }
-    if (!L.segs[d].empty() && nwd0 == L.segs[d].size()) C->wd_mode[d] = kModeUpdateWd0;
+    if (!L.segs[d].empty() && nwd0 == L.segs[d].size() && (d != FKS_F32 || FKS_WD0_F32_MODE))
+      C->wd_mode[d] = kModeUpdateWd0;
     else if (!L.segs[d].empty() && nwd == L.segs[d].size()) C->wd_mode[d] = kModeUpdateWd;
     else if (!L.segs[d].empty() && nwd == 0) C->wd_mode[d] = kModeUpdateNoWd;
   }
