@@ -519,7 +519,7 @@ void key_put(std::vector<uint8_t>& k, const T& v) {
 }
 
 #ifndef FKS_WD0_F32_MODE
-#define FKS_WD0_F32_MODE 1  // fp32 launches with wd = +-0 take kModeUpdateWd0 (0: kModeUpdateWd, the same bits)
+#define FKS_WD0_F32_MODE 0  // fp32 launches with wd = +-0 take kModeUpdateWd0 (1) or kModeUpdateWd (0, the same bits: 2.21 vs 2.28 ms per 19-seed launch, profiles/r02n_ab_f32wd0.log)
 #endif
 std::vector<uint8_t> plan_key(const fks_tensor* t, int nt, const double* scales, uint64_t delta_base, int shard,
                               int nshards, bool small) {
