@@ -340,7 +340,11 @@ def run(args, world, rank, local):
                 "frac": round(ach / VALU_PEAK_TLANEOPS, 4),
                 "mix_ceiling": round(VALU_MIX_CEILING_TLANEOPS, 2),
                 "frac_of_mix_ceiling": round(ach / VALU_MIX_CEILING_TLANEOPS, 4),
-                "traffic": None,
+                # HBM bytes per launch from the PMC passes (FETCH_SIZE + WRITE_SIZE, corrected as
+                # MI355X_MICROARCH.md prescribes; tools/summarize_pmc2.py)
+                "traffic": (round(pmc["hbm_bytes_per_param_per_launch"] * rank_params)
+                            if pmc.get("hbm_bytes_per_param_per_launch") else None),
+                "traffic_unit": "HBM bytes per launch",
                 "kernel": "fks_apply_bs_kernel", "launches": prof.n_apply,
                 "avg_launch_ms": round(prof.apply_ms / n_apply, 3),
                 "units_per_launch": units, "lane_ops_per_unit": round(lane_ops, 3),
