@@ -2,7 +2,7 @@
 the 7B bf16 K=4096 reconstruct for N = 1, 2, 4, 8 (the work each rank of an N-GPU run
 does; ranks share nothing on the data path).  Predicts the driver's strong-scaling
 efficiency t_1 / (N t_N) up to the max-over-ranks skew.
-python tools/shard_rank_time.py [--ns 1,2,4,8]"""
+python tools/shard_rank_time.py [--ns 1,2,4,8] [--wd 0.0]"""
 import argparse
 import json
 import os
@@ -21,6 +21,7 @@ import bench  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ns", default="1,2,4,8")
+    ap.add_argument("--wd", type=float, default=0.0, help="weight decay (bench.py's default 0.0)")
     args = ap.parse_args()
     from fate_llm.algo.fedkseed import codec
     dev = torch.device("cuda", 0)
@@ -31,7 +32,7 @@ def main():
     for s in shapes:
         views.append(flat[off:off + bench.numel(s)].view(s))
         off += bench.numel(s)
-    specs = [codec.ParamSpec(v, lr=1e-5, weight_decay=0.01) for v in views]
+    specs = [codec.ParamSpec(v, lr=1e-5, weight_decay=args.wd) for v in views]
     seeds, vals = bench.synthetic_seeds(4096)
     keep = [(s, v) for s, v in zip(seeds, vals) if v != 0.0]
     ks, kv = [s for s, _ in keep], [v for _, v in keep]
@@ -45,7 +46,7 @@ def main():
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         t1 = t1 or dt * n
-        print(json.dumps({"nshards": n, "rank0_s": round(dt, 3), "apply_s": round(prof.apply_ms / 1e3, 3),
+        print(json.dumps({"wd": args.wd, "nshards": n, "rank0_s": round(dt, 3), "apply_s": round(prof.apply_ms / 1e3, 3),
                           "jump_s": round(prof.jump_ms / 1e3, 3),
                           "predicted_efficiency": round(t1 / (n * dt), 4)}), flush=True)
 
