@@ -90,6 +90,9 @@
 #ifndef FKS_WD0_F32
 #define FKS_WD0_F32 1  // the zero-weight-decay fma form also in the fp32 kernels (0: the full chain there)
 #endif
+#ifndef FKS_JUMP_W10
+#define FKS_JUMP_W10 1  // jump kernel: 63 lanes x 10 words per chunk state instead of 52 x 12 (0.305 -> 0.288 s per 7B K=4096 reconstruct, profiles/r02r_shard_*.log)
+#endif
 #ifndef FKS_BS_ROLEMAP
 #define FKS_BS_ROLEMAP 0  // slice kernel: wave roles (0: twist waves 5 and 11, on SIMDs 1 and 3; 1: 5 and 9, both on SIMD 1 beside one pair wave: +5 %, profiles/r02i_ab.log)
 #endif
@@ -424,6 +427,47 @@ __device__ __forceinline__ void jump_pair_step(uint32_t (&acc)[12], uint32_t w0,
       : "scc");
 }
 
+// The same for 10 words per lane (FKS_JUMP_W10: 63 lanes x 10 words cover the 624 state
+// words, so 63 of 64 lanes work instead of 52): acc[j] ^= c0 * w[j] ^ c1 * w[j + 1], j < 10.
+__device__ __forceinline__ void jump_pair_step10(uint32_t (&acc)[10], uint32_t w0, uint32_t w1, uint32_t w2,
+                                                 uint32_t w3, uint32_t w4, uint32_t w5, uint32_t w6, uint32_t w7,
+                                                 uint32_t w8, uint32_t w9, uint32_t w10, uint32_t two) {
+  asm volatile(
+      "s_cmp_eq_u32 %[two], 0\n\t"
+      "s_cbranch_scc1 .Lkend%=\n\t"
+      "s_cmp_eq_u32 %[two], 3\n\t"
+      "s_cbranch_scc1 .Lkboth%=\n\t"
+      "s_cmp_eq_u32 %[two], 1\n\t"
+      "s_cbranch_scc1 .Lkone%=\n\t"
+      "v_xor_b32 %0, %0, %[w1]\n\tv_xor_b32 %1, %1, %[w2]\n\tv_xor_b32 %2, %2, %[w3]\n\t"
+      "v_xor_b32 %3, %3, %[w4]\n\tv_xor_b32 %4, %4, %[w5]\n\tv_xor_b32 %5, %5, %[w6]\n\t"
+      "v_xor_b32 %6, %6, %[w7]\n\tv_xor_b32 %7, %7, %[w8]\n\tv_xor_b32 %8, %8, %[w9]\n\t"
+      "v_xor_b32 %9, %9, %[w10]\n\t"
+      "s_branch .Lkend%=\n"
+      ".Lkone%=:\n\t"
+      "v_xor_b32 %0, %0, %[w0]\n\tv_xor_b32 %1, %1, %[w1]\n\tv_xor_b32 %2, %2, %[w2]\n\t"
+      "v_xor_b32 %3, %3, %[w3]\n\tv_xor_b32 %4, %4, %[w4]\n\tv_xor_b32 %5, %5, %[w5]\n\t"
+      "v_xor_b32 %6, %6, %[w6]\n\tv_xor_b32 %7, %7, %[w7]\n\tv_xor_b32 %8, %8, %[w8]\n\t"
+      "v_xor_b32 %9, %9, %[w9]\n\t"
+      "s_branch .Lkend%=\n"
+      ".Lkboth%=:\n\t"
+      "v_bitop3_b32 %0, %0, %[w0], %[w1] bitop3:0x96\n\tv_bitop3_b32 %1, %1, %[w1], %[w2] bitop3:0x96\n\t"
+      "v_bitop3_b32 %2, %2, %[w2], %[w3] bitop3:0x96\n\tv_bitop3_b32 %3, %3, %[w3], %[w4] bitop3:0x96\n\t"
+      "v_bitop3_b32 %4, %4, %[w4], %[w5] bitop3:0x96\n\tv_bitop3_b32 %5, %5, %[w5], %[w6] bitop3:0x96\n\t"
+      "v_bitop3_b32 %6, %6, %[w6], %[w7] bitop3:0x96\n\tv_bitop3_b32 %7, %7, %[w7], %[w8] bitop3:0x96\n\t"
+      "v_bitop3_b32 %8, %8, %[w8], %[w9] bitop3:0x96\n\tv_bitop3_b32 %9, %9, %[w9], %[w10] bitop3:0x96\n"
+      ".Lkend%=:"
+      : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]),
+        "+v"(acc[7]), "+v"(acc[8]), "+v"(acc[9])
+      : [w0] "v"(w0), [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4), [w5] "v"(w5), [w6] "v"(w6),
+        [w7] "v"(w7), [w8] "v"(w8), [w9] "v"(w9), [w10] "v"(w10), [two] "s"(two)
+      : "scc");
+}
+__device__ __forceinline__ uint4 lds_b64x2(const uint32_t* p) {  // 8-byte aligned: two ds_read_b64
+  const uint2 lo = *reinterpret_cast<const uint2*>(p), hi = *reinterpret_cast<const uint2*>(p + 2);
+  return make_uint4(lo.x, lo.y, hi.x, hi.y);
+}
+
 __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_j[];
   uint32_t* xs = lds_j + kJumpXOff;
@@ -448,27 +492,35 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
     __syncthreads();
   }
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const uint32_t* yb = xs + 1 + 12 * lane;  // y[12 lane]
+#if FKS_JUMP_W10
+  constexpr int kW = 10, kLanes = 63;  // 63 lanes x 10 words (lane 62 keeps words 620..623)
+#else
+  constexpr int kW = 12, kLanes = kJumpLanes;
+#endif
+  const uint32_t* yb = xs + 1 + kW * lane;  // y[kW lane]
   const int c0 = blockIdx.y * a.chunks_per_wg;
   const int c1 = min(c0 + a.chunks_per_wg, a.nchunks);
   for (int c = c0 + wave; c < c1; c += kJumpThreads / 64) {
     const int64_t b = a.chunk_block[c];
-    uint32_t acc[12];
+    uint32_t acc[kW];
 #pragma unroll
-    for (int j = 0; j < 12; j++) acc[j] = 0u;
-    if (lane < kJumpLanes) {
+    for (int j = 0; j < kW; j++) acc[j] = 0u;
+    if (lane < kLanes) {
       if (b == 0) {
 #pragma unroll
-        for (int j = 0; j < 12; j++) acc[j] = xs[12 * lane + j];
+        for (int j = 0; j < kW; j++) acc[j] = kW * lane + j < kMtN ? xs[kW * lane + j] : 0u;
       } else {
         const uint64_t* poly = a.polys + (size_t)c * 312;  // wave-uniform: scalar loads
         uint32_t win[16];
         {
-          const uint4 q0 = lds_b128(yb), q1 = lds_b128(yb + 4), q2 = lds_b128(yb + 8);
+#if FKS_JUMP_W10
+          const uint4 q0 = lds_b64x2(yb), q1 = lds_b64x2(yb + 4), q2 = lds_b64x2(yb + 8), q3 = lds_b64x2(yb + 12);
+#else
+          const uint4 q0 = lds_b128(yb), q1 = lds_b128(yb + 4), q2 = lds_b128(yb + 8), q3 = lds_b128(yb + 12);
+#endif
           win[0] = q0.x; win[1] = q0.y; win[2] = q0.z; win[3] = q0.w;
           win[4] = q1.x; win[5] = q1.y; win[6] = q1.z; win[7] = q1.w;
           win[8] = q2.x; win[9] = q2.y; win[10] = q2.z; win[11] = q2.w;
-          const uint4 q3 = lds_b128(yb + 12);
           win[12] = q3.x; win[13] = q3.y; win[14] = q3.z; win[15] = q3.w;
         }
         uint64_t next = poly[0];
@@ -479,8 +531,12 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
           const uint32_t* yw = yb + 64 * wd;
 #pragma unroll
           for (int q = 0; q < 16; q++) {
-            // window = y[64 wd + 4q + 12 lane + 0..15], stored rotated by 4q (mod 16)
+            // window = y[64 wd + 4q + kW lane + 0..15], stored rotated by 4q (mod 16)
+#if FKS_JUMP_W10
+            const uint4 nx = lds_b64x2(yw + 4 * q + 16);
+#else
             const uint4 nx = lds_b128(yw + 4 * q + 16);
+#endif
             const int rot = (4 * q) & 15;
             const uint32_t word = q < 8 ? lo : hi;
 #pragma unroll
@@ -490,11 +546,18 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
               // per word (v_bitop3), so a random polynomial costs 0.75 instead of 2
               // VALU ops per word and coefficient pair
               const uint32_t two = (word >> ((4 * q + d) & 31)) & 3u;
+#if FKS_JUMP_W10
+              jump_pair_step10(acc, win[(rot + d) & 15], win[(rot + d + 1) & 15], win[(rot + d + 2) & 15],
+                               win[(rot + d + 3) & 15], win[(rot + d + 4) & 15], win[(rot + d + 5) & 15],
+                               win[(rot + d + 6) & 15], win[(rot + d + 7) & 15], win[(rot + d + 8) & 15],
+                               win[(rot + d + 9) & 15], win[(rot + d + 10) & 15], two);
+#else
               jump_pair_step(acc, win[(rot + d) & 15], win[(rot + d + 1) & 15], win[(rot + d + 2) & 15],
                              win[(rot + d + 3) & 15], win[(rot + d + 4) & 15], win[(rot + d + 5) & 15],
                              win[(rot + d + 6) & 15], win[(rot + d + 7) & 15], win[(rot + d + 8) & 15],
                              win[(rot + d + 9) & 15], win[(rot + d + 10) & 15], win[(rot + d + 11) & 15],
                              win[(rot + d + 12) & 15], two);
+#endif
             }
             win[(rot + 0) & 15] = nx.x;
             win[(rot + 1) & 15] = nx.y;
@@ -503,9 +566,15 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
           }
         }
       }
-      uint32_t* out = a.states + ((size_t)k * a.nchunks + c) * kMtN + 12 * lane;
+      uint32_t* out = a.states + ((size_t)k * a.nchunks + c) * kMtN + kW * lane;
+#if FKS_JUMP_W10
 #pragma unroll
-      for (int j = 0; j < 12; j += 4) *reinterpret_cast<uint4*>(out + j) = make_uint4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
+      for (int j = 0; j < kW; j += 2)
+        if (kW * lane + j < kMtN) *reinterpret_cast<uint2*>(out + j) = make_uint2(acc[j], acc[j + 1]);
+#else
+#pragma unroll
+      for (int j = 0; j < kW; j += 4) *reinterpret_cast<uint4*>(out + j) = make_uint4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
+#endif
     }
   }
 }
