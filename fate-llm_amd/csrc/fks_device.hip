@@ -1783,7 +1783,10 @@ constexpr int kBsStateBytes = 8 * kBsChunkBytes;       // 79,872
 // dword (4 B, ds_read_b32): a random 8-bit-indexed ds_read_b64 measured 17.4 CU-cycles per
 // wave-instruction against 6.5 for ds_read_b32 (tools/ubench/issue2.hip), for two unpack ops
 constexpr int kBsCsBytes = 8;                          // room for either layout
-constexpr int kBsTabBytes = 256 * 4 + 256 * kBsCsBytes;  // 3,072
+// FKS_BS_PLANAR: the S table 1024 B after C (one ds_read2st64_b32 for both) or, PLANAR 2,
+// 1028 B after (no read2 form reaches it: two ds_read_b32)
+constexpr int kBsSTabOff = FKS_BS_PLANAR == 2 ? 2052 : 2048;
+constexpr int kBsTabBytes = FKS_BS_PLANAR == 2 ? 3088 : 256 * 4 + 256 * kBsCsBytes;  // 3,072
 template <int MODE>
 constexpr bool bs_cspack() {
   return !FKS_BS_PLANAR &&
@@ -1914,7 +1917,7 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
     reinterpret_cast<float*>((uint8_t*)lds32)[i] = c_tab_bf16[i];
     if (FKS_BS_PLANAR) {
       reinterpret_cast<float*>((uint8_t*)lds32 + 1024)[i] = c_tab_bf16[256 + i];
-      reinterpret_cast<float*>((uint8_t*)lds32 + 2048)[i] = c_tab_bf16[512 + i];
+      reinterpret_cast<float*>((uint8_t*)lds32 + kBsSTabOff)[i] = c_tab_bf16[512 + i];
     } else if (bs_cspack<MODE>())  // C in the low half, S in the high half (both exact bf16 values)
       reinterpret_cast<uint32_t*>((uint8_t*)lds32 + 1024)[i] =
           (__float_as_uint(c_tab_bf16[256 + i]) >> 16) | (__float_as_uint(c_tab_bf16[512 + i]) & 0xffff0000u);
@@ -2037,7 +2040,7 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
     const float r = lds_f32(ia);
     rr = f32x2_t{r, r};
     if (FKS_BS_PLANAR) {  // C[b] and S[b] 1024 B apart: one ds_read2st64_b32
-      cs = f32x2_t{lds_f32(1024u + ib), lds_f32(2048u + ib)};
+      cs = f32x2_t{lds_f32(1024u + ib), lds_f32((uint32_t)kBsSTabOff + ib)};
     } else if (bs_cspack<MODE>()) {
       const uint32_t w = lds_u32((int)(1024u + ib));
       cs = f32x2_t{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
