@@ -97,7 +97,7 @@
 #define FKS_BS_ROLEMAP 0  // slice kernel: wave roles (0: twist waves 5 and 11, on SIMDs 1 and 3; 1: 5 and 9, both on SIMD 1 beside one pair wave: +5 %, profiles/r02i_ab.log)
 #endif
 #ifndef FKS_BS_PLANAR
-#define FKS_BS_PLANAR 0  // slice kernel: C and S as two f32 tables 1 KB apart, one ds_read2st64_b32 per seed (measured +19 % at wd 0.0, +8 % at wd 0.01: profiles/r02j_ab_planar.log)
+#define FKS_BS_PLANAR 0  // slice kernel: C and S as two f32 tables 1 KB apart, one ds_read2st64_b32 per seed (measured +19 % at wd 0.0, +8 % at wd 0.01: profiles/r02j_ab_planar.log); 2: two ds_read_b32 (+24 %, r02u_ab_planar2.log)
 #endif
 #ifndef FKS_BS_CSPACK
 // slice kernel: (C,S) table as packed bf16 pairs (ds_read_b32, two unpack ops) instead of f32 pairs
