@@ -126,15 +126,41 @@ print(json.dumps({"done": done, "s": time.perf_counter() - t0}))
 '''
 
 
+def usable_cpus():
+    """CPUs this process may actually run on: its affinity mask, capped by a cgroup CPU
+    quota (v2 cpu.max or v1 cfs_quota_us) -- on a GPU box the job's CPU share, which can
+    be far below os.cpu_count() (the whole host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        n = min(n, max(1, int(quota)))
+    return max(1, n), quota
+
+
 def cpu_baseline(budget_s, wd):
     """The reference's CPU path (torch.manual_seed + torch.normal + the update expression
-    of zo_utils.py:49, re-typed in oracle/torch_replica.py) on bounded samples of the
+    of zo_utils.py:47-52, re-typed in oracle/torch_replica.py) on bounded samples of the
     same workload, scaled linearly to the 7B buffer x the 4055 non-zero seeds of K=4096:
       * one process at torch's default thread count, at two sizes (2^22 and 2^24 bf16
         params) to check linearity in N;
-      * the all-core variant: P = min(16, cores) single-thread processes over disjoint
-        seeds (torch.normal holds the generator mutex, so one process draws on one
-        core), the fairest CPU upper bound -- reported as `value`."""
+      * the all-core variant -- reported as `value`: one single-thread process per CPU this
+        job may use (affinity mask and cgroup quota, usable_cpus) over disjoint seeds
+        (torch.normal holds the generator mutex, so one process draws on one core), the
+        fairest CPU upper bound.  `cores` = processes run; `nproc` = the host's CPU count;
+        when the job's share is smaller than the host, `all_host_cores_extrapolated`
+        scales the measured per-process rate to every host core (not measured)."""
     from oracle import torch_replica as R
     threads = torch.get_num_threads()
     seeds, scalars = synthetic_seeds(4096)
@@ -153,10 +179,10 @@ def cpu_baseline(budget_s, wd):
 
     ns_small, d_small, _ = one_process(1 << 22, budget_s * 0.2)
     ns_big, d_big, dt_big = one_process(1 << 24, budget_s * 0.3)
-    procs = max(1, min(16, os.cpu_count() or 1))
+    procs, quota = usable_cpus()
     n_all = 1 << 22
-    env = dict(os.environ, FKS_ROOT=ROOT, N=str(n_all), WD="none" if wd is None else repr(wd), STEP=str(procs), BUDGET=str(int(max(2, budget_s * 0.5))),
-               OMP_NUM_THREADS="1")
+    env = dict(os.environ, FKS_ROOT=ROOT, N=str(n_all), WD="none" if wd is None else repr(wd), STEP=str(procs),
+               BUDGET=str(int(max(2, budget_s * 0.5))), OMP_NUM_THREADS="1")
     kids = [subprocess.Popen([sys.executable, "-c", _CPU_CHILD], env=dict(env, FIRST=str(i)), stdout=subprocess.PIPE,
                              text=True) for i in range(procs)]
     outs = [json.loads(k.communicate()[0].strip().splitlines()[-1]) for k in kids]
@@ -165,20 +191,30 @@ def cpu_baseline(budget_s, wd):
     ns_all = wall / (n_all * done_all) * 1e9  # aggregate: ns per seed*param over all processes
     t7b = LLAMA7B_PARAMS * t7b_seeds * ns_all * 1e-9
     t7b_one = LLAMA7B_PARAMS * t7b_seeds * ns_big * 1e-9
-    return {
-        "value": LLAMA7B_PARAMS * 2 / t7b / 1e9, "unit": "GB/s", "cores": procs, "kind": "port",
+    nproc = os.cpu_count() or procs
+    value = LLAMA7B_PARAMS * 2 / t7b / 1e9
+    out = {
+        "value": value, "unit": "GB/s", "cores": procs, "kind": "port",
         "sample": (f"torch CPU replica of zo_utils.directional_derivative_step (oracle/torch_replica.py, "
                    f"weight_decay {wd}), "
-                   f"{procs} single-thread processes over disjoint seeds: {done_all} seeds x {n_all} bf16 params in "
-                   f"{wall:.1f} s = {ns_all:.3f} ns per seed*param aggregate, scaled linearly to 6.74e9 params x "
-                   f"{t7b_seeds} non-zero seeds ({t7b / 3600:.1f} h)"),
+                   f"{procs} single-thread processes (one per usable CPU) over disjoint seeds: {done_all} seeds x "
+                   f"{n_all} bf16 params in {wall:.1f} s = {ns_all:.3f} ns per seed*param aggregate, scaled linearly "
+                   f"to 6.74e9 params x {t7b_seeds} non-zero seeds ({t7b / 3600:.1f} h)"),
         "single_process": {"threads": threads, "ns_per_seed_param_2^22": round(ns_small, 3),
                            "ns_per_seed_param_2^24": round(ns_big, 3), "seeds_2^22": d_small, "seeds_2^24": d_big,
                            "seconds_2^24": round(dt_big, 1), "value_GBps": LLAMA7B_PARAMS * 2 / t7b_one / 1e9,
                            "note": "torch.normal single-threaded under the generator mutex; elementwise ops on "
                                    f"{threads} threads; the two sizes check linearity in N"},
-        "nproc": os.cpu_count(),
+        "nproc": nproc,
+        "usable_cpus": {"affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+                        "cgroup_quota_cpus": quota},
     }
+    if procs < nproc:
+        out["all_host_cores_extrapolated"] = {
+            "value": value * nproc / procs, "cores": nproc,
+            "note": (f"this job may use {procs} of the host's {nproc} CPUs (affinity / cgroup quota); the measured "
+                     "per-process rate x every host core, assuming perfect scaling -- an upper bound, not measured")}
+    return out
 
 
 # ------------------------------------------------------------------ launcher
@@ -332,8 +368,17 @@ def run(args, world, rank, local):
     seeds_per_launch = rank_seeds * n_steps_prof / n_apply
     units = rank_params * seeds_per_launch  # seed*param updates per launch
     pmc = load_pmc_summary(wd)
+    from fate_llm.algo.fedkseed import _native
+    build_id = _native.build_id()
     lane_ops = pmc.get("valu_lane_ops_per_seed_param")
     valu = None
+    withheld = None
+    if lane_ops and pmc.get("build_id") != build_id:
+        # the committed counters were profiled from other device code: their lane-ops per
+        # unit do not describe the kernels timed here
+        withheld = (f"profiles/{pmc_summary_name(wd)} was profiled from libfks.so build {pmc.get('build_id')}, "
+                    f"this run loaded build {build_id}: VALU roofline withheld (re-run tools/gpu_pmc2.sh)")
+        lane_ops = None
     if lane_ops and not seed_shard:
         ach = units * lane_ops / avg_apply_s / 1e12
         valu = {"bound": "valu", "achieved": round(ach, 3), "peak": round(VALU_PEAK_TLANEOPS, 2), "unit": "Tlane-op/s",
@@ -348,6 +393,7 @@ def run(args, world, rank, local):
                 "kernel": "fks_apply_bs_kernel", "launches": prof.n_apply,
                 "avg_launch_ms": round(prof.apply_ms / n_apply, 3),
                 "units_per_launch": units, "lane_ops_per_unit": round(lane_ops, 3),
+                "build_id": build_id,
                 "counters": {k: pmc.get(k) for k in ("valu_active_frac", "valu_dual_issue_frac", "wait_any_frac",
                                                      "lds_bank_conflict_frac", "clock_ghz")},
                 "unit_def": ("one seed*param update (z draw + update chain); lane-ops = rocprofv3 SQ_INSTS_VALU x 64 "
@@ -364,7 +410,7 @@ def run(args, world, rank, local):
     traffic = pmc.get("hbm_bytes_per_param_per_launch")
     hbm = {"bound": "hbm", "achieved": round(hbm_ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(hbm_ach / HBM_PEAK_GBS, 7),
-           "traffic": (round(traffic * rank_params) if traffic and not seed_shard else None),
+           "traffic": (round(traffic * rank_params) if traffic and not seed_shard and not withheld else None),
            "alg_bytes_per_step": alg_bytes_step,
            "per_pass": {"alg_bytes_per_launch": 2 * rank_params * elt,
                         "achieved_GBps": round(2 * rank_params * elt / avg_apply_s / 1e9, 2),
@@ -385,12 +431,15 @@ def run(args, world, rank, local):
                    "parallelism": f"seed-shard{world}" if seed_shard else f"element-shard{world}"},
         "roofline": valu if valu else hbm,
         "roofline_hbm": hbm,
+        "build_id": build_id,
         "jump_kernel_ms_per_step": round(prof.jump_ms / n_steps_prof, 2),
     }
     if world > 1:
         out["backend"] = dist.get_backend()
         if share:
             out["shared_gpu"] = True  # a rehearsal, not a measurement
+    if withheld:
+        out["valu_roofline_withheld"] = withheld
     if gather_ms is not None:
         out["gather_ms"] = round(gather_ms, 1)
     if alt is not None:

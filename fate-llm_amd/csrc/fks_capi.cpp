@@ -467,8 +467,9 @@ struct CachedPlan {
 // the seed and the block's stream position, not on the tensors, so any later one-seed
 // call with the same seed and the same bf16 segment ranges (a store covers the blocks of
 // its own bf16 segments only) whose regular blocks lie inside the stored range replays them.
-// 1 byte per parameter of device memory; allocated only while it is a small share of the
-// free memory (FKS_ZCACHE=0 turns it off).  Stream hand-off by event, as WinCache.
+// The buffer is the CALLER's (fks_zindex_attach: the Python codec allocates it through
+// torch's allocator under a memory budget), 1 byte per parameter; without one attached,
+// or with FKS_ZCACHE=0, every call generates.  Stream hand-off by event, as WinCache.
 struct ZCache {
   int device = -1;
   void* buf = nullptr;
@@ -685,59 +686,42 @@ void clear_plan_cache() {
     if (W.buf) (void)hipFree(W.buf);
     if (W.done) (void)hipEventDestroy(W.done);
   }
-  for (ZCache& Z : g_zc) {
+  for (ZCache& Z : g_zc) {  // the caller's buffers stay attached; their contents are dropped
     (void)hipSetDevice(Z.device);
     (void)hipDeviceSynchronize();
-    if (Z.buf) (void)hipFree(Z.buf);
-    if (Z.done) (void)hipEventDestroy(Z.done);
+    Z.valid = false;
+    Z.stream = nullptr;
   }
   (void)hipSetDevice(cur);
   g_win.clear();
-  g_zc.clear();
 }
 
-// The z-index cache of the current device, ordered after its last user on `stream`,
-// with room for `bytes` (allocated if the free memory allows), or nullptr.
+// The z-index cache entry of the current device (created on first use), or nullptr if
+// its event cannot be created.  Caller holds g_cache_mu.
+ZCache* z_entry() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  for (ZCache& z : g_zc)
+    if (z.device == dev) return z.done ? &z : nullptr;
+  g_zc.emplace_back();
+  ZCache* Z = &g_zc.back();
+  Z->device = dev;
+  if (hipEventCreateWithFlags(&Z->done, hipEventDisableTiming) != hipSuccess) {
+    Z->done = nullptr;
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return Z;
+}
+
+// The z-index cache of the current device, ordered after its last user on `stream`, if
+// the attached buffer holds `bytes`; nullptr otherwise (the call then generates).
 ZCache* z_cache(void* stream, size_t bytes) {
   const char* env = std::getenv("FKS_ZCACHE");
   if (env && env[0] == '0') return nullptr;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  ZCache* Z = nullptr;
-  for (ZCache& z : g_zc)
-    if (z.device == dev) Z = &z;
-  if (!Z) {
-    g_zc.emplace_back();
-    Z = &g_zc.back();
-    Z->device = dev;
-    if (hipEventCreateWithFlags(&Z->done, hipEventDisableTiming) != hipSuccess) {
-      Z->done = nullptr;
-      (void)hipGetLastError();
-    }
-  }
-  if (!Z->done) return nullptr;
-  if (Z->bytes < bytes) {
-    if (Z->buf) {
-      if (hipEventSynchronize(Z->done) != hipSuccess) return nullptr;
-      (void)hipFree(Z->buf);
-      Z->buf = nullptr;
-      Z->bytes = 0;
-    }
-    Z->valid = false;
-    size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
-      (void)hipGetLastError();
-      return nullptr;
-    }
-    // a small share of what is free: the parameters' owner keeps its headroom
-    if (bytes + std::max<size_t>(total_b / 10, (size_t)4 << 30) > free_b) return nullptr;
-    if (hipMalloc(&Z->buf, bytes) != hipSuccess) {
-      Z->buf = nullptr;
-      (void)hipGetLastError();
-      return nullptr;
-    }
-    Z->bytes = bytes;
-  } else if (Z->stream && Z->stream != stream) {
+  ZCache* Z = z_entry();
+  if (!Z || !Z->buf || Z->bytes < bytes) return nullptr;
+  if (Z->stream && Z->stream != stream) {
     if (hipStreamWaitEvent((hipStream_t)stream, Z->done, 0) != hipSuccess) return nullptr;
   }
   Z->stream = stream;
@@ -1018,6 +1002,34 @@ int fks_workspace_size(const fks_tensor* t, int32_t nt, int32_t k, size_t* bytes
     validate(t, nt);
     if (!bytes || k < 0) throw Error(-FKS_EINVAL, "bad arguments");
     *bytes = workspace_total(t, nt, k, 0);
+  });
+}
+
+int fks_zindex_size(const fks_tensor* t, int32_t nt, size_t* bytes) {
+  return guarded([&] {
+    validate(t, nt);
+    if (!bytes) throw Error(-FKS_EINVAL, "bad arguments");
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    const CachedPlan* C = get_plan(t, nt, nullptr, 0, 0, 1, true);
+    *bytes = (C->have_reg && C->nsegs[FKS_BF16] > 0)
+                 ? (size_t)kSm2ZidxBytesPerBlock * (size_t)(C->reg_hi - C->reg_lo)
+                 : 0;
+  });
+}
+
+int fks_zindex_attach(void* buf, size_t bytes) {
+  return guarded([&] {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    ZCache* Z = z_entry();
+    if (!Z) throw Error(-FKS_EHIP, "z-index cache event");
+    // the last call that used the old buffer may still be running: the caller may free
+    // or reuse it once this returns
+    if (Z->buf && Z->stream && hipEventSynchronize(Z->done) != hipSuccess)
+      throw Error(-FKS_EHIP, "z-index cache: waiting for the last user");
+    Z->buf = bytes ? buf : nullptr;
+    Z->bytes = buf ? bytes : 0;
+    Z->valid = false;
+    Z->stream = nullptr;
   });
 }
 

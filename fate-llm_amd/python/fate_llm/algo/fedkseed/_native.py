@@ -25,7 +25,8 @@ EXPORTED = (
     "fks_abi_version", "fks_build_target", "fks_host_jump_window", "fks_host_tables",
     "fks_directional_step_shard", "fks_stream_length", "fks_profile_begin", "fks_profile_end",
     "fks_shard_census", "fks_perturb_step", "fks_delta_workspace_size", "fks_delta_accumulate", "fks_delta_apply",
-    "fks_plan_cache_clear", "fks_perturb_step_dev", "fks_device_selfcheck",
+    "fks_plan_cache_clear", "fks_perturb_step_dev", "fks_device_selfcheck", "fks_build_id",
+    "fks_zindex_size", "fks_zindex_attach",
 )
 
 
@@ -69,6 +70,7 @@ def load():
         L.fks_last_error.restype = ctypes.c_char_p
         L.fks_abi_version.restype = c_i32
         L.fks_build_target.restype = ctypes.c_char_p
+        L.fks_build_id.restype = ctypes.c_char_p
         L.fks_host_jump_window.argtypes = [c_u64, ctypes.c_int64, P]
         L.fks_host_tables.argtypes = [c_i32, P, P, P, c_i32]
         L.fks_directional_step_shard.argtypes = [P, c_i32, P, P, c_i32, c_i32, c_i32, c_i32, P, c_sz, P]
@@ -84,16 +86,23 @@ def load():
         L.fks_plan_cache_clear.argtypes = []
         L.fks_perturb_step_dev.argtypes = [P, c_i32, c_u64, P, P, P, c_sz, P]
         L.fks_device_selfcheck.argtypes = [c_i32, ctypes.POINTER(c_u64), P, c_sz, P]
+        L.fks_zindex_size.argtypes = [P, c_i32, ctypes.POINTER(c_sz)]
+        L.fks_zindex_attach.argtypes = [P, c_sz]
         for name in ("fks_workspace_size", "fks_directional_step", "fks_perturb", "fks_normal",
                      "fks_host_jump_window", "fks_host_tables", "fks_directional_step_shard",
                      "fks_stream_length", "fks_profile_begin", "fks_profile_end", "fks_shard_census", "fks_perturb_step",
                      "fks_delta_workspace_size", "fks_delta_accumulate", "fks_delta_apply", "fks_plan_cache_clear",
-                     "fks_perturb_step_dev", "fks_device_selfcheck"):
+                     "fks_perturb_step_dev", "fks_device_selfcheck", "fks_zindex_size", "fks_zindex_attach"):
             getattr(L, name).restype = ctypes.c_int
         if L.fks_abi_version() != ABI_VERSION:
             raise OSError(f"libfks.so ABI {L.fks_abi_version()} != {ABI_VERSION}")
         _lib = L
         return L
+
+
+def build_id() -> str:
+    """16 hex digits identifying the device code of the loaded libfks.so (fks_build_id)."""
+    return load().fks_build_id().decode()
 
 
 def check(rc: int) -> None:

@@ -22,6 +22,8 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
+import threading
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -135,6 +137,52 @@ def directional_step(specs: Sequence[ParamSpec], seeds: Sequence[int], values: S
         b.finish()
 
 
+# ---------------------------------------------------------------- z-index buffer
+# A one-seed bf16 perturb stores its Box-Muller table indices (1 byte per parameter) so
+# that the zeroth-order step's second and third calls with the same seed replay them
+# (include/fks.h, fks_zindex_attach).  The buffer is a torch tensor -- it counts in
+# torch.cuda.memory_allocated and goes back to torch's allocator on release -- and is
+# taken only while it stays within ZINDEX_BUDGET_FRAC of the device's memory (the
+# parameters' owner keeps the rest for activations); FKS_ZCACHE=0 turns it off.
+ZINDEX_BUDGET_FRAC = float(os.environ.get("FKS_ZINDEX_BUDGET_FRAC", "0.05"))
+_zindex = {}  # device index -> attached uint8 tensor
+_zindex_lock = threading.Lock()
+
+
+def zindex_reserve(b: "_Batch") -> bool:
+    """Attach a z-index buffer big enough for one-seed calls over ``b`` on its device, if
+    the budget allows; returns whether one is attached."""
+    if os.environ.get("FKS_ZCACHE", "1").startswith("0") or ZINDEX_BUDGET_FRAC <= 0:
+        return False
+    L = N.load()
+    need = ctypes.c_size_t(0)
+    N.check(L.fks_zindex_size(ctypes.addressof(b.arr), b.n, ctypes.byref(need)))
+    need = int(need.value)
+    if need == 0:
+        return False
+    idx = b.device.index if b.device.index is not None else torch.cuda.current_device()
+    with _zindex_lock:
+        cur = _zindex.get(idx)
+        if cur is not None and cur.numel() >= need:
+            return True
+        if need > ZINDEX_BUDGET_FRAC * torch.cuda.get_device_properties(idx).total_memory:
+            return False
+        buf = torch.empty(need, dtype=torch.uint8, device=b.device)
+        N.check(L.fks_zindex_attach(buf.data_ptr(), need))  # waits for the old buffer's last user
+        _zindex[idx] = buf
+        return True
+
+
+def zindex_release(device=None) -> None:
+    """Detach and free the z-index buffer of ``device`` (all devices if None)."""
+    L = N.load()
+    with _zindex_lock:
+        for idx in [d for d in _zindex if device is None or d == torch.device(device).index]:
+            with torch.cuda.device(idx):
+                N.check(L.fks_zindex_attach(None, 0))
+            del _zindex[idx]
+
+
 def perturb(tensors: Sequence[torch.Tensor], seed: int, scales) -> None:
     """p <- p + scale_i*z for every tensor i (scale = scaling_factor*eps of its group, a
     python double); ``scales`` is one number for all tensors or one per tensor."""
@@ -151,6 +199,7 @@ def perturb(tensors: Sequence[torch.Tensor], seed: int, scales) -> None:
     L = N.load()
     sc = np.ascontiguousarray([float(x) for x in scales], dtype=np.float64)
     with torch.cuda.device(b.device):
+        zindex_reserve(b)
         ws, nbytes = b.workspace(1)
         N.check(L.fks_perturb(ctypes.addressof(b.arr), b.n, _seed_u64(seed), sc.ctypes.data, ws.data_ptr(), nbytes,
                               _stream_handle(b.device)))

@@ -107,17 +107,22 @@ _STAGES = 3
 
 
 def _h2d_staged(pairs, device) -> None:
-    """dst.copy_(src) for every (device dst, host src) pair, through _STAGES pinned
-    buffers on a side stream; pinned sources go straight to the DMA.  The current stream
-    waits for the copies (the caller's next kernels see the data)."""
+    """dst.copy_(src) for every (device dst, source) pair, through _STAGES pinned
+    buffers on a side stream; pinned and device sources go straight to the DMA.  The side
+    stream first waits for the current stream (the destinations were allocated there, and
+    their memory's previous owner or a device source's producer may still have work
+    queued on it); the current stream then waits for the copies (the caller's next kernels
+    see the data)."""
+    cur = torch.cuda.current_stream(device)
     stream = torch.cuda.Stream(device)
+    stream.wait_stream(cur)
     bufs, ready = [], [None] * _STAGES
     i = 0
     with torch.cuda.stream(stream):
         for dst, src in pairs:
             if src.numel() == 0:
                 continue
-            if src.is_pinned():
+            if src.is_pinned() or src.device.type == "cuda":
                 dst.copy_(src, non_blocking=True)
                 continue
             s = src.contiguous().view(-1).view(torch.uint8)
@@ -134,7 +139,7 @@ def _h2d_staged(pairs, device) -> None:
                 ready[slot] = torch.cuda.Event()
                 ready[slot].record(stream)
                 i += 1
-    torch.cuda.current_stream(device).wait_stream(stream)
+    cur.wait_stream(stream)
     stream.synchronize()  # the staging buffers are released on return
 
 

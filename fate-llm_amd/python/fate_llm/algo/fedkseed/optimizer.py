@@ -99,12 +99,21 @@ class ZerothOrderOptimizer(RandomWalkOptimizer):
         codec.perturb_step(specs, directional_derivative_seed, scales, float(g), value_is_tensor=True, update=True)
         return g, loss_right, loss_left
 
+    # loss dtypes whose g reaches the kernels exactly as an f32 (then rounded to each
+    # parameter's dtype there, as the host path's 0-dim tensor value is)
+    _DEVICE_LOSS_DTYPES = (torch.float32, torch.bfloat16, torch.float16)
+
     def _on_device(self, loss_right, loss_left) -> bool:
+        """The device tail takes exactly the losses the host path treats as a 0-dim tensor
+        value (zo_utils._value_kind): 0-dim f32 / bf16 / f16 tensors on the parameters'
+        device.  Anything else (a shape-(1,) loss, an f64 loss) goes through the host
+        path, which accepts and rejects the same inputs as the reference."""
         if not (self.device_step and self._fusable()):
             return False
         dev = next((p.device for group in self.param_groups for p in group["params"]), None)
         return (dev is not None and dev.type == "cuda" and all(
-            isinstance(x, torch.Tensor) and x.device == dev and x.numel() == 1 for x in (loss_right, loss_left)))
+            isinstance(x, torch.Tensor) and x.device == dev and x.dim() == 0 and x.dtype in self._DEVICE_LOSS_DTYPES
+            for x in (loss_right, loss_left)))
 
     def _device_tail(self, seed, loss_right, loss_left):
         """optimizer.py:136-148 without leaving the device: g = (loss_right - loss_left) /

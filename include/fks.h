@@ -24,10 +24,12 @@
  * Conventions (all entry points):
  *  - plain pointers and sizes only; tensor data are DEVICE pointers, contiguous,
  *    aligned to the element size; seeds/values are HOST arrays;
- *  - the caller owns the parameters and the workspace (a device buffer of at least
- *    fks_workspace_size() bytes); the library's only allocations are its bounded
- *    plan cache of per-layout headers (see fks_plan_cache_clear) -- evicting an entry
- *    synchronises the device that owns it -- and the per-device __constant__ tables;
+ *  - the caller owns the parameters, the workspace (a device buffer of at least
+ *    fks_workspace_size() bytes) and the optional z-index buffer (fks_zindex_attach);
+ *    the library's only device allocations are its bounded plan cache of per-layout
+ *    headers (see fks_plan_cache_clear) -- evicting an entry synchronises the device
+ *    that owns it --, the one-seed calls' window cache (624 words per chunk of
+ *    2,048: about 5 MB) and the per-device __constant__ tables;
  *  - asynchronous on `stream` (a hipStream_t; NULL = default stream), like torch ops;
  *  - return 0 on success or a negative errno-style code; fks_last_error() gives a
  *    thread-local message; no C++ exception crosses the ABI;
@@ -131,13 +133,23 @@ int fks_profile_end(double* apply_ms, int64_t* n_apply, double* jump_ms, int64_t
  * freed by fks_plan_cache_clear; FKS_NO_WIN_CACHE in the environment turns it off.
  *
  * One-seed bf16 perturbs also store the Box-Muller table indices of every MT block they
- * cover (1 byte per parameter, a library-owned per-device buffer, allocated only while
- * it stays a small share of the free device memory): a later one-seed perturb /
- * perturb_step / K=1 update with the same seed over blocks inside that range replays
- * the indices instead of running the generator -- the zeroth-order step's second and
- * third calls, a streaming pass at 5 B of HBM traffic per parameter.  Values are
- * identical either way; FKS_ZCACHE=0 turns it off; fks_plan_cache_clear frees it. */
+ * cover in the z-index buffer the CALLER attached to the current device (fks_zindex_attach):
+ * a later one-seed perturb / perturb_step / K=1 update with the same seed over blocks
+ * inside that range replays the indices instead of running the generator -- the
+ * zeroth-order step's second and third calls, a streaming pass at 5 B of HBM traffic per
+ * parameter.  Values are identical either way; without an attached buffer of
+ * fks_zindex_size bytes (or with FKS_ZCACHE=0) every call generates.  fks_plan_cache_clear
+ * drops the buffer's contents, not the attachment. */
 int fks_plan_cache_clear(void);
+
+/* Bytes of z-index buffer a one-seed call over this tensor list stores (0: the list has no
+ * bf16 fast segments).  Host-side; builds / reuses the list's plan. */
+int fks_zindex_size(const fks_tensor* t, int32_t nt, size_t* bytes);
+/* Attach `bytes` of caller-owned device memory on the current device as its z-index
+ * buffer (NULL or 0 detaches).  Returns after the last call that used the previously
+ * attached buffer has finished on the device, so the caller may then free or reuse it.
+ * The library keeps the pointer until the next attach; it never frees it. */
+int fks_zindex_attach(void* buf, size_t bytes);
 
 /* torch.manual_seed(seed); for every tensor i in order: p = p + scales[i]*z, where
  * scales[i] = scaling_factor*eps of the tensor's group, computed in double by the
@@ -197,6 +209,11 @@ const char* fks_last_error(void);
 /* ABI version (FKS_ABI_VERSION) and the device target the library was built for. */
 int32_t fks_abi_version(void);
 const char* fks_build_target(void);
+/* Identity of the device code in this library: 16 hex digits of the SHA-256 of the
+ * compiled kernel object (fate-llm_amd/Makefile).  Hardware counters profiled from one
+ * build (profiles/pmc_*.json) carry it, so a report can check that they belong to the
+ * kernels it times (bench.py). */
+const char* fks_build_id(void);
 
 /* Host-only self checks (no device needed): the jump-ahead window of `seed` at
  * stream block `block` (= the 624-word generator state before block `block` is

@@ -40,13 +40,16 @@ def test_world_size_mismatch_fails_loudly():
     assert "WORLD_SIZE" in r.stderr
 
 
-def test_cpu_baseline_leg_runs():
+@pytest.mark.parametrize("wd", [0.0, None])
+def test_cpu_baseline_leg_runs(wd):
     sys.path.insert(0, ROOT)
     import bench
 
-    cb = bench.cpu_baseline(3.0, 0.0)
+    cb = bench.cpu_baseline(3.0, wd)
     assert cb["kind"] == "port" and cb["unit"] == "GB/s" and cb["value"] > 0
-    assert 1 <= cb["cores"] <= 16
+    # one single-thread process per CPU this job may use; the host's count beside it
+    assert cb["cores"] == bench.usable_cpus()[0] and cb["nproc"] == os.cpu_count()
+    assert ("all_host_cores_extrapolated" in cb) == (cb["cores"] < cb["nproc"])
     sp = cb["single_process"]
     # linear in N: the per-(seed*param) cost at 2^22 and 2^24 params agrees within 2x
     assert 0.5 < sp["ns_per_seed_param_2^22"] / sp["ns_per_seed_param_2^24"] < 2.0

@@ -36,6 +36,7 @@ def test_header_symbols_exported():
         assert hasattr(L, name), name
     assert L.fks_abi_version() == N.ABI_VERSION
     assert L.fks_build_target() == b"gfx950"
+    assert re.fullmatch(r"[0-9a-f]{16}", N.build_id())
 
 
 def test_fks_tensor_layout_matches_header():

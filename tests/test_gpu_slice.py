@@ -87,3 +87,27 @@ def test_slice_element_shards_equal_oracle(nshards):
     O.reconstruct(arrays, [O.BF16] * 3, [1e-3] * 3, [0.01] * 3, seeds, vals)
     for i, (t, a) in enumerate(zip(ts, arrays)):
         assert_bitwise(to_np(t), a, "bfloat16", f"tensor {i}")
+
+
+@pytest.mark.parametrize("k", [32, 95])
+@pytest.mark.parametrize("wd", [0.0, None])
+def test_slice_multiblock_chunks_vs_oracle(k, wd):
+    """The regime of every 7B launch: each of the slice kernel's 512 chunks spans many MT
+    blocks, so the twist wave carries block b into b + 1 inside a chunk (the bench's
+    chain: weight decay 0.0 -> kModeUpdateWd0, None -> kModeUpdateNoWd, both with the
+    packed (C,S) table).  4.2 M bf16 params = 6,771 MT blocks (13 per chunk); K = 32 is
+    one full pass, K = 95 three passes with a partial one.  Bit-exact against the oracle
+    (fedkseed.py:136-141, zo_utils.py:47-52)."""
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    shapes = [1 << 22, 624 * 48 + 32]
+    arrays = rand_params(shapes, "bfloat16", seed=1000 + k)
+    seeds, vals = _seeds(k, seed=2000 + k)
+    ts = [from_np(a, "bfloat16", dev) for a in arrays]
+    assert codec.stream_length(ts) // 624 >= 8 * 512, "fewer than 8 MT blocks per chunk"
+    specs = [codec.ParamSpec(t, lr=1e-5, weight_decay=wd) for t in ts]
+    codec.directional_step(specs, seeds, vals)
+    torch.cuda.synchronize()
+    O.reconstruct(arrays, [O.BF16] * len(arrays), [1e-5] * len(arrays), [wd] * len(arrays), seeds, vals)
+    for i, (t, a) in enumerate(zip(ts, arrays)):
+        assert_bitwise(to_np(t), a, "bfloat16", f"K={k} wd={wd} tensor {i}")

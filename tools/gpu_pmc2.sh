@@ -13,6 +13,9 @@ for v in ${VARIANTS:-full}; do
   if [ "$v" = "wd0" ]; then unset FKS_LIB_OVERRIDE; export PERF_WD=0.0
   elif [ "$v" != "full" ]; then export FKS_LIB_OVERRIDE=$PWD/fate-llm_amd/build/libfks_$v.so; unset PERF_WD
   else unset FKS_LIB_OVERRIDE; unset PERF_WD; fi
+  # the device-code identity of the library these passes profile (summarize_pmc2.py records it)
+  python3 -c 'import sys; sys.path.insert(0, "fate-llm_amd/python"); from fate_llm.algo.fedkseed import _native; print(_native.build_id())' \
+    > gpurun_out/pmc2_${v}_buildid || exit 97
   i=0
   for g in "${GROUPS_[@]}"; do
     rm -rf gpurun_out/pmc2_${v}_$i

@@ -46,7 +46,14 @@ def main(tag, variant, params, seeds, kernel=None, elt=2):
     c = {k: sum(v) / len(v) for k, v in c.items()}  # GRBM_GUI_ACTIVE appears in several passes
     units = params * seeds
     clk_cycles = c["GRBM_GUI_ACTIVE"] / 8  # summed over the 8 XCDs
+    try:
+        build_id = open(f"gpurun_out/pmc2_{variant}_buildid").read().strip()
+    except OSError:
+        build_id = None
     out = {
+        # fks_build_id() of the profiled libfks.so: bench.py uses these counters only for
+        # a library with the same device code
+        "build_id": build_id,
         "source": f"rocprofv3 --pmc passes (tools/perf_one.py, {params} params of {elt} B, "
                   f"{seeds}-seed launches), variant {variant}; dispatches per pass {sorted(set(n_disp.values()))}",
         "kernel": kernel or "fks_apply_bs_kernel<MODE,true>", "seeds_per_full_launch": seeds, "params": params,
