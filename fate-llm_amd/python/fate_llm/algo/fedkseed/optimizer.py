@@ -14,7 +14,7 @@ from torch.optim import Optimizer
 
 from . import codec
 from .pytorch_utils import get_optimizer_parameters_grouped_with_decay
-from .zo_utils import directional_derivative_step
+from .zo_utils import _value_kind, directional_derivative_step
 
 
 class RandomWalkOptimizer(Optimizer):
@@ -93,10 +93,17 @@ class ZerothOrderOptimizer(RandomWalkOptimizer):
             self.random_perturb_parameters(directional_derivative_seed, scaling_factor=1.0)
             g = self.directional_derivative_step(directional_derivative_seed, g)
             return g, loss_right, loss_left
-        torch.manual_seed(directional_derivative_seed)
         specs = codec.resolve_groups(self.param_groups)
+        try:
+            # the same value rules as the unfused directional step (a g that would rebind
+            # param.data to another dtype or shape is rejected), checked before any update
+            v, is_tensor = _value_kind(g, specs)
+        except NotImplementedError:
+            self.random_perturb_parameters(directional_derivative_seed, scaling_factor=1.0)
+            raise
+        torch.manual_seed(directional_derivative_seed)
         scales = [1.0 * group["eps"] for group in self.param_groups for _ in group["params"]]
-        codec.perturb_step(specs, directional_derivative_seed, scales, float(g), value_is_tensor=True, update=True)
+        codec.perturb_step(specs, directional_derivative_seed, scales, v, value_is_tensor=is_tensor, update=True)
         return g, loss_right, loss_left
 
     # loss dtypes whose g reaches the kernels exactly as an f32 (then rounded to each
