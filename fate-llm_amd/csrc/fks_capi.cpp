@@ -159,9 +159,14 @@ void validate(const fks_tensor* t, int nt) {
     const size_t es = elem_size(x.dtype);
     if (x.numel > 0 && (!x.data || ((uintptr_t)x.data % es) != 0))
       throw Error(-FKS_EINVAL, "tensor " + std::to_string(i) + ": null or misaligned data pointer");
-    if (x.flags & ~(FKS_HAS_WD | FKS_FROZEN)) throw Error(-FKS_EINVAL, "tensor " + std::to_string(i) + ": unknown flags");
+    if (x.flags & ~(FKS_HAS_WD | FKS_FROZEN | FKS_STREAM_ROCM))
+      throw Error(-FKS_EINVAL, "tensor " + std::to_string(i) + ": unknown flags");
+    if ((x.flags & FKS_STREAM_ROCM) != (t[0].flags & FKS_STREAM_ROCM))
+      throw Error(-FKS_EINVAL, "tensor " + std::to_string(i) + ": every tensor of a call must use the same z stream");
   }
 }
+
+bool rocm_stream(const fks_tensor* t, int nt) { return nt > 0 && (t[0].flags & FKS_STREAM_ROCM) != 0; }
 
 // Chunk plan: MT blocks [chunk_block[c], chunk_block[c+1]) per workgroup.
 struct Plan {
@@ -519,9 +524,9 @@ void key_put(std::vector<uint8_t>& k, const T& v) {
   k.insert(k.end(), p, p + sizeof(T));
 }
 
-#ifndef FKS_WD0_F32_MODE
-#define FKS_WD0_F32_MODE 0  // fp32 launches with wd = +-0 take kModeUpdateWd0 (1) or kModeUpdateWd (0, the same bits: 2.21 vs 2.28 ms per 19-seed launch, profiles/r02n_ab_f32wd0.log)
-#endif
+// fp32 launches with wd = +-0 keep kModeUpdateWd (the same bits as kModeUpdateWd0, and
+// 2.21 vs 2.28 ms per 19-seed launch: profiles/r02n_ab_f32wd0.log)
+constexpr bool kWd0F32Mode = false;
 std::vector<uint8_t> plan_key(const fks_tensor* t, int nt, const double* scales, uint64_t delta_base, int shard,
                               int nshards, bool small) {
   std::vector<uint8_t> k;
@@ -593,7 +598,7 @@ CachedPlan* build_plan(const fks_tensor* t, int nt, const double* scales, uint64
       nwd += (sg.flags & FKS_HAS_WD) ? 1 : 0;
       nwd0 += ((sg.flags & FKS_HAS_WD) && sg.wd == 0.0f) ? 1 : 0;  // +0.0 or -0.0
     }
-    if (!L.segs[d].empty() && nwd0 == L.segs[d].size() && (d != FKS_F32 || FKS_WD0_F32_MODE))
+    if (!L.segs[d].empty() && nwd0 == L.segs[d].size() && (d != FKS_F32 || kWd0F32Mode))
       C->wd_mode[d] = kModeUpdateWd0;
     else if (!L.segs[d].empty() && nwd == L.segs[d].size()) C->wd_mode[d] = kModeUpdateWd;
     else if (!L.segs[d].empty() && nwd == 0) C->wd_mode[d] = kModeUpdateNoWd;
@@ -674,10 +679,32 @@ CachedPlan* get_plan(const fks_tensor* t, int nt, const double* scales, uint64_t
   return C;
 }
 
+struct PhxPlan {
+  std::vector<uint8_t> key;
+  uint64_t hash = 0, last_use = 0;
+  void* dev = nullptr;
+  int device = 0;
+  int nt = 0;           // table entries (tensors with work items)
+  int64_t items = 0;    // work items of all tensors
+};
+std::vector<PhxPlan*> g_phx;
+
+void free_phx(PhxPlan* P) {
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (P->device != cur) (void)hipSetDevice(P->device);
+  (void)hipDeviceSynchronize();
+  (void)hipFree(P->dev);
+  if (P->device != cur) (void)hipSetDevice(cur);
+  delete P;
+}
+
 void clear_plan_cache() {
   std::lock_guard<std::mutex> lk(g_cache_mu);
   for (CachedPlan* C : g_cache) free_plan(C);
   g_cache.clear();
+  for (PhxPlan* P : g_phx) free_phx(P);
+  g_phx.clear();
   int cur = 0;
   (void)hipGetDevice(&cur);
   for (WinCache& W : g_win) {
@@ -775,7 +802,110 @@ WinCache* win_cache(void* stream, size_t bytes) {
 // LDS): enough workgroups to cover every CU before packing chunks into fewer groups.
 int jump_chunks_per_wg(int nseeds, int nchunks) {
   const int per_cu = (int)(((int64_t)nseeds * nchunks + device_cu_count() - 1) / device_cu_count());
-  return std::max(1, std::min({FKS_JUMP_MAX_CPW, per_cu, nchunks}));
+  return std::max(1, std::min({kJumpMaxCpw, per_cu, nchunks}));
+}
+
+// ------------------------------------------------------------------ torch_rocm stream
+// The tensor table of a FKS_STREAM_ROCM call (PhxTensor, fks_internal.h), resident on the
+// device once per distinct tensor list (same key as the MT plans, bounded LRU, freed by
+// fks_plan_cache_clear).  The geometry is torch's calc_execution_policy
+// (ATen/native/cuda/DistributionTemplates.h:50-62) on this device.
+PhxPlan* get_phx_plan(const fks_tensor* t, int nt, const double* scales) {
+  std::vector<uint8_t> key = plan_key(t, nt, scales, 0, 0, 1, false);
+  key_put(key, (int)0x7068);  // "ph": not an MT plan key
+  key_put(key, device_max_threads_per_cu());
+  const uint64_t h = fnv1a(key);
+  for (PhxPlan* P : g_phx)
+    if (P->hash == h && P->key == key) {
+      P->last_use = ++g_cache_clock;
+      return P;
+    }
+  const int64_t max_grid = (int64_t)device_cu_count() * (device_max_threads_per_cu() / 256);
+  std::vector<PhxTensor> tab;
+  uint64_t off4 = 0;
+  int64_t items = 0;
+  for (int i = 0; i < nt; i++) {
+    const int64_t n = t[i].numel;
+    if (n == 0) continue;  // torch draws nothing for an empty tensor (the offset stays)
+    if (n * (int64_t)elem_size(t[i].dtype) > (int64_t)INT32_MAX)
+      throw Error(-FKS_ENOTSUP, "tensor " + std::to_string(i) +
+                                    ": torch_rocm stream of a tensor past 2^31 bytes (torch splits its draw) is not supported");
+    const int64_t grid = std::min<int64_t>((n + 255) / 256, max_grid);
+    const int64_t stride = 256 * grid;
+    const int64_t J = (n - 1) / (4 * stride) + 1;  // loop iterations = philox offset increment / 4
+    if (!(t[i].flags & FKS_FROZEN)) {
+      PhxTensor x{};
+      x.ptr = (uint64_t)(uintptr_t)t[i].data;
+      x.numel = n;
+      x.item0 = items;
+      x.off4 = off4;
+      x.stride = (uint32_t)stride;
+      x.dtype = t[i].dtype;
+      x.lr = t[i].lr;
+      x.wd = t[i].wd;
+      x.flags = t[i].flags & FKS_HAS_WD;
+      x.ps = scales ? (float)scales[i] : 0.0f;
+      tab.push_back(x);
+      items += stride * J;
+    }
+    off4 += (uint64_t)J;
+  }
+  auto* P = new PhxPlan();
+  P->key = std::move(key);
+  P->hash = h;
+  P->last_use = ++g_cache_clock;
+  P->nt = (int)tab.size();
+  P->items = items;
+  (void)hipGetDevice(&P->device);
+  const size_t bytes = std::max<size_t>(sizeof(PhxTensor) * tab.size(), 256);
+  if (hipMalloc(&P->dev, bytes) != hipSuccess) {
+    delete P;
+    throw Error(-FKS_ENOMEM, "torch_rocm plan hipMalloc");
+  }
+  if (!tab.empty() && hipMemcpy(P->dev, tab.data(), sizeof(PhxTensor) * tab.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(P->dev);
+    delete P;
+    throw Error(-FKS_EHIP, "torch_rocm plan upload");
+  }
+  if (g_phx.size() >= kPlanCacheEntries) {
+    auto victim = std::min_element(g_phx.begin(), g_phx.end(),
+                                   [](const PhxPlan* a, const PhxPlan* b) { return a->last_use < b->last_use; });
+    free_phx(*victim);
+    g_phx.erase(victim);
+  }
+  g_phx.push_back(P);
+  return P;
+}
+
+// the torch_rocm stream: seeds in passes of kBsSeeds (by value in the kernel arguments);
+// element shards split the work items
+void run_philox(const fks_tensor* t, int nt, const uint64_t* seeds, const double* values, int k, int value_kind,
+                int mode, void* stream, const double* scales, int shard, int nshards, const float* gdev) {
+  if (mode != kModeUpdate && mode != kModePerturb && mode != kModePerturbUpdate && mode != kModeWriteZ)
+    throw Error(-FKS_ENOTSUP, "the torch_rocm stream supports the reconstruct, perturb and normal calls only");
+  std::lock_guard<std::mutex> lk(g_cache_mu);
+  const PhxPlan* P = get_phx_plan(t, nt, scales);
+  if (P->nt == 0 || P->items == 0) return;
+  PhiloxArgs a{};
+  a.t = static_cast<const PhxTensor*>(P->dev);
+  a.nt = P->nt;
+  a.gdev = gdev;
+  a.mode = mode;
+  a.item_lo = (int64_t)((__int128)P->items * shard / nshards);
+  a.item_hi = (int64_t)((__int128)P->items * (shard + 1) / nshards);
+  if (a.item_lo >= a.item_hi) return;
+  for (int s0 = 0; s0 < k; s0 += kPhxSeeds) {
+    const int nb = std::min(kPhxSeeds, k - s0);
+    for (int j = 0; j < nb; j++) {
+      a.seeds[j] = seeds[s0 + j];
+      for (int d = 0; d < 3; d++)
+        a.g[3 * j + d] = value_kind == FKS_VALUE_TENSOR ? round_to_dtype(values[s0 + j], d) : (float)values[s0 + j];
+    }
+    a.nseeds = nb;
+    const int rc = timed(0, stream, [&] { return launch_philox(a, stream); });
+    if (rc) throw Error(rc < 0 ? rc : -FKS_EHIP, std::string("fks_philox_kernel launch: ") +
+                                                     (rc > 0 ? hipGetErrorString((hipError_t)rc) : "unsupported"));
+  }
 }
 
 void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* values, int k, int value_kind, int mode,
@@ -787,6 +917,10 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
   if (value_kind != FKS_VALUE_SCALAR && value_kind != FKS_VALUE_TENSOR)
     throw Error(-FKS_EINVAL, "bad value_kind");
   if (k == 0 || nt == 0) return;
+  if (rocm_stream(t, nt)) {
+    run_philox(t, nt, seeds, values, k, value_kind, mode, stream, tensor_scales, shard, nshards, gdev);
+    return;
+  }
   const bool small = k <= kSmallK;
   std::lock_guard<std::mutex> lk(g_cache_mu);  // no eviction while this call uses its entry
   const CachedPlan* C = get_plan(t, nt, tensor_scales, delta_base, shard, nshards, small);
@@ -1009,6 +1143,10 @@ int fks_zindex_size(const fks_tensor* t, int32_t nt, size_t* bytes) {
   return guarded([&] {
     validate(t, nt);
     if (!bytes) throw Error(-FKS_EINVAL, "bad arguments");
+    if (rocm_stream(t, nt)) {  // the z-index cache serves the CPU stream only
+      *bytes = 0;
+      return;
+    }
     std::lock_guard<std::mutex> lk(g_cache_mu);
     const CachedPlan* C = get_plan(t, nt, nullptr, 0, 0, 1, true);
     *bytes = (C->have_reg && C->nsegs[FKS_BF16] > 0)
@@ -1091,6 +1229,7 @@ int fks_delta_apply(const fks_tensor* t, int32_t nt, const float* delta, const d
 namespace fks {
 namespace {
 size_t workspace_total(const fks_tensor* t, int nt, int k, uint64_t delta_base) {
+  if (rocm_stream(t, nt)) return kWsStatesOff;  // counter-mode: no generator windows
   // upper bound over every shard count: a shard never needs more chunks than the whole
   // stream; the header itself lives in the plan cache, not in the workspace
   const Layout L = make_layout(t, nt, nullptr, delta_base);

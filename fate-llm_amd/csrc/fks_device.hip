@@ -25,99 +25,13 @@
 #include "fks_internal.h"
 #include "fks_bitslice.h"
 
-#ifndef FKS_DIAG
-#define FKS_DIAG 0  // diagnostic builds only (make diag): timing variants with wrong results
-#endif
-#ifndef FKS_STAGED
-#define FKS_STAGED 0  // bf16 pair phase: all indices, then all lookups, then all products
-#endif
-#ifndef FKS_UNROLL2
-#define FKS_UNROLL2 0  // apply block loop unrolled by two (slots swap roles)
-#endif
-#ifndef FKS_T64
-#define FKS_T64 1  // bf16 pair tempering on the 64-bit word pair (v_lshrrev_b64 / v_lshlrev_b64)
-#endif
-#ifndef FKS_BS_DIAG
-#define FKS_BS_DIAG 0  // slice kernel diagnostics (wrong results): 1 no twist, 2 no pair chain, 3 no lookups,
-                        // 5 no barriers in the block loop, 6 twist without stores, 7 twist without loads
-#endif
-#ifndef FKS_DB_MIN_WAVES
-#define FKS_DB_MIN_WAVES 4  // launch-bounds waves per SIMD of the double-buffered small-K kernel (6 WGs/CU measured 19 % slower than 5 at any bound)
-#endif
-#ifndef FKS_ZR_GRID
-#define FKS_ZR_GRID 1  // z-index replay: grid-stride tiles (1) or one chunk per workgroup (0)
-#endif
-#ifndef FKS_ZR_UNROLL
-#define FKS_ZR_UNROLL 2  // z-index replay: tiles per loop iteration (in flight per wave)
-#endif
-#ifndef FKS_SM2_TWREG
-#define FKS_SM2_TWREG 1  // small-K twist wave: phases chained in registers (twist_oop_reg)
-#endif
-#ifndef FKS_SM2_TAB
-#define FKS_SM2_TAB 0  // small-K kernel bf16 table layout: 0 R|(C,S) f32x2, 1 R|C|S f32, 2 R|(C,S) packed bf16
-#endif
-#ifndef FKS_SM2_MIN_WAVES
-#define FKS_SM2_MIN_WAVES 8  // launch-bounds waves per SIMD of fks_small2_kernel (8 workgroups of 4 waves per CU: <= 64 VGPRs)
-#endif
-#ifndef FKS_SMALL_DBUF
-#define FKS_SMALL_DBUF 1  // passes of <= kSmallK seeds: double-buffered windows, twist overlapped
-#endif
-#ifndef FKS_BS_PAIR_PRIO
-#define FKS_BS_PAIR_PRIO 1  // slice kernel: s_setprio of the pair waves (1: 6 % faster than 0)
-#endif
-#ifndef FKS_BS_PRIO
-#define FKS_BS_PRIO 0  // slice kernel: s_setprio of the twist wave
-#endif
-#ifndef FKS_BS_TAIL
-#define FKS_BS_TAIL 0  // slice kernel: seeds of a block run after barrier 2, over the next rows' reads (0: measured best; 4/8/12 put the twist on the critical path: +9 / +15 / +25 %)
-#endif
-#ifndef FKS_BS_FENCE
-#define FKS_BS_FENCE 8  // slice kernel: compiler fence after every FKS_BS_FENCE seeds' table lookups (0: none)
-#endif
-#ifndef FKS_BS_LA
-#define FKS_BS_LA 0  // slice kernel: table-lookup lookahead in seeds (0: compiler-scheduled, each seed's reads waited with lgkmcnt(0); pinned pipelines of 1/2/3/4/6/8 seeds measured +6.7/+1.2/-0.3/+1.2/+2.9/+4.9 %, profiles/r02f_ab_la.log)
-#endif
-#ifndef FKS_BS_SCHED
-#define FKS_BS_SCHED 1  // slice kernel lookahead: scheduling barriers pin the software pipeline's order
-#endif
-#if FKS_BS_SCHED
-// the machine scheduler otherwise hoists a seed's z product right under its own table
-// reads (which then wait lgkmcnt(0) for the whole LDS latency)
-#define FKS_BS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define FKS_BS_SCHED_FENCE() asm volatile("" ::: "memory")
-#endif
-#ifndef FKS_WD0_F32
-#define FKS_WD0_F32 1  // the zero-weight-decay fma form also in the fp32 kernels (0: the full chain there)
-#endif
-#ifndef FKS_JUMP_W10
-#define FKS_JUMP_W10 1  // jump kernel: 63 lanes x 10 words per chunk state instead of 52 x 12 (0.305 -> 0.288 s per 7B K=4096 reconstruct, profiles/r02r_shard_*.log)
-#endif
-#ifndef FKS_BS_ROLEMAP
-#define FKS_BS_ROLEMAP 0  // slice kernel: wave roles (0: twist waves 5 and 11, on SIMDs 1 and 3; 1: 5 and 9, both on SIMD 1 beside one pair wave: +5 %, profiles/r02i_ab.log)
-#endif
-#ifndef FKS_BS_PLANAR
-#define FKS_BS_PLANAR 0  // slice kernel: C and S as two f32 tables 1 KB apart, one ds_read2st64_b32 per seed (measured +19 % at wd 0.0, +8 % at wd 0.01: profiles/r02j_ab_planar.log); 2: two ds_read_b32 (+24 %, r02u_ab_planar2.log)
-#endif
-#ifndef FKS_BS_CSPACK
-// slice kernel: (C,S) table as packed bf16 pairs (ds_read_b32, two unpack ops) instead of f32 pairs
-// (ds_read_b64): 0 never, 1 always, 2 for the chains without the weight-decay roundings
-// (kModeUpdateWd0 / NoWd: 3.84 vs 4.03 ms per launch, profiles/r02g_ab_wd0.log)
-#define FKS_BS_CSPACK 2
-#endif
-#ifndef FKS_F32_RSQRT
-#define FKS_F32_RSQRT 0  // fp32 radius: 1 = v_sqrt_f32 + one residual step, no denormal scaling
-                         // (fewer instructions, measured 4 % slower: 1.74 vs 1.67 ps per seed*param)
-#endif
-#ifndef FKS_F32_FAST
-#define FKS_F32_FAST 1  // fp32 z: pair tempering and the domain-exact sincos / fma rewrites (z_pair_f32_raw)
-#endif
-#ifndef FKS_TEMPER_FOLD
-#define FKS_TEMPER_FOLD 1  // bf16 pair tempering with the third step folded into the index (temper_pair_u8x8)
-#endif
-#ifndef FKS_RPAIR
-#define FKS_RPAIR 0  // radius table as (R,R) pairs read with ds_read_b64 (1) or one dword of the pair at the x8 index (2); 0: R[256] f32, ds_read_b32
-#endif
+// Design choices measured on MI355X in rounds 1-2 are fixed in the code; the A/B knobs
+// and the wrong-result timing diagnostics of those rounds were removed (their logs are
+// under profiles/, their code in the git history).
+constexpr int kDbMinWaves = 4;   // launch-bounds waves per SIMD of the double-buffered small-K kernel (6 WGs/CU measured 19 % slower than 5)
+constexpr int kZrUnroll = 2;     // z-index replay: tiles per loop iteration (in flight per wave)
+constexpr int kSm2MinWaves = 8;  // launch-bounds waves per SIMD of fks_small2_kernel (8 workgroups of 4 waves per CU: <= 64 VGPRs)
+constexpr int kBsFence = 8;      // slice kernel: compiler fence after every 8 seeds' table lookups
 
 namespace fks {
 namespace {
@@ -140,22 +54,6 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
   return y;
 }
 
-// low 8 bits of the tempered word (the bf16 uniform), times 4 (a byte offset into a
-// 256-entry f32 table): ((y ^ (y >> 18)) & 0xFF) << 2 = ((y << 2) ^ (y >> 16)) & 0x3FC
-__device__ __forceinline__ uint32_t mt_temper_u8x4(uint32_t y) {
-  y ^= (y >> 11);
-  y = __builtin_amdgcn_bitop3_b32(y, y << 7, 0x9d2c5680u, kXorAnd);
-  y = __builtin_amdgcn_bitop3_b32(y, y << 15, 0xefc60000u, kXorAnd);
-  return __builtin_amdgcn_bitop3_b32(y << 2, y >> 16, 0x3FCu, kXorMask);
-}
-
-// the same bits times 8 (a byte offset into a table of f32 pairs)
-__device__ __forceinline__ uint32_t mt_temper_u8x8(uint32_t y) {
-  y ^= (y >> 11);
-  y = __builtin_amdgcn_bitop3_b32(y, y << 7, 0x9d2c5680u, kXorAnd);
-  y = __builtin_amdgcn_bitop3_b32(y, y << 15, 0xefc60000u, kXorAnd);
-  return __builtin_amdgcn_bitop3_b32(y << 3, y >> 15, 0x7F8u, kXorMask);
-}
 
 // ------------------------------------------------------------------ rounding
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
@@ -166,15 +64,7 @@ __device__ __forceinline__ float rbf_cvt(float x) {
   const f32x2_t v = {0.0f, x};
   return __builtin_bit_cast(float, __builtin_convertvector(v, bf16x2_t));
 }
-__device__ __forceinline__ float rbf(float x) {
-#if FKS_DIAG == 5  // diagnostics: truncation instead of RNE (wrong values)
-  return __uint_as_float(__float_as_uint(x) & 0xffff0000u);
-#elif FKS_DIAG == 7  // diagnostics: no rounding at all (wrong values)
-  return x;
-#else
-  return rbf_cvt(x);
-#endif
-}
+__device__ __forceinline__ float rbf(float x) { return rbf_cvt(x); }
 __device__ __forceinline__ float rhf(float x) {  // RNE to f16 and back
   // The empty asm pins x as an f32 VALUE: without it the backend folds the producing
   // f32 multiply into v_fma_mixlo_f16 (one rounding of the exact product straight to
@@ -222,55 +112,6 @@ __device__ __forceinline__ float cephes_logf(float x) {  // x in [2^-24, 1]
   return x;
 }
 
-__device__ __forceinline__ void cephes_sincosf(float xin, float& s, float& c) {
-  uint32_t sign_bit_sin = __float_as_uint(xin) & 0x80000000u;
-  float x = __uint_as_float(__float_as_uint(xin) & 0x7fffffffu);
-  float y = x * 1.27323954473516f;
-  int32_t imm2 = (int32_t)y;  // cvttps: truncation
-  imm2 = (imm2 + 1) & ~1;
-  y = (float)imm2;
-  const int32_t imm4 = imm2 - 2;
-  const uint32_t swap_sign_bit_sin = ((uint32_t)(imm2 & 4)) << 29;
-  const bool poly_mask = (imm2 & 2) == 0;
-  x = __fmaf_rn(y, -0.78515625f, x);
-  x = __fmaf_rn(y, -2.4187564849853515625e-4f, x);
-  x = __fmaf_rn(y, -3.77489497744594108e-8f, x);
-  const uint32_t sign_bit_cos = ((uint32_t)(~imm4 & 4)) << 29;
-  sign_bit_sin ^= swap_sign_bit_sin;
-  const float z = x * x;
-  float yc = 2.443315711809948E-005f;
-  yc = __fmaf_rn(yc, z, -1.388731625493765E-003f);
-  yc = __fmaf_rn(yc, z, 4.166664568298827E-002f);
-  yc = yc * z;
-  yc = __fmaf_rn(yc, z, -(z * 0.5f));
-  yc = yc + 1.0f;
-  float ys = -1.9515295891E-4f;
-  ys = __fmaf_rn(ys, z, 8.3321608736E-3f);
-  ys = __fmaf_rn(ys, z, -1.6666654611E-1f);
-  ys = ys * z;
-  ys = __fmaf_rn(ys, x, x);
-  const float ysin2 = poly_mask ? ys : 0.0f;
-  const float ysin1 = poly_mask ? 0.0f : yc;
-  ys = ys - ysin2;
-  yc = yc - ysin1;
-  const float xmm1 = ysin1 + ysin2;
-  const float xmm2 = yc + ys;
-  s = __uint_as_float(__float_as_uint(xmm1) ^ sign_bit_sin);
-  c = __uint_as_float(__float_as_uint(xmm2) ^ sign_bit_cos);
-}
-
-// z pair (element j, element j+8) from the two tempered words of a 16-block
-__device__ __forceinline__ void z_pair_f32(uint32_t w1, uint32_t w2, float& z1, float& z2) {
-  const float d1 = (float)(w1 & 0xFFFFFFu) * (1.0f / 16777216.0f);  // uniform_real<float>
-  const float d2 = (float)(w2 & 0xFFFFFFu) * (1.0f / 16777216.0f);
-  const float u1 = 1.0f - d1;
-  const float radius = sqrtf(-2.0f * cephes_logf(u1));  // _mm256_sqrt_ps: correctly rounded
-  const float theta = 6.28318548202514648438f * d2;      // (float)(2.0f * c10::pi<double>)
-  float s, c;
-  cephes_sincosf(theta, s, c);
-  z1 = radius * c + 0.0f;  // _mm256_fmadd_ps(n1, std=1, mean=0)
-  z2 = radius * s + 0.0f;
-}
 
 // ------------------------------------------------------------------ per-dtype traits
 template <int DT>
@@ -372,63 +213,22 @@ __device__ __forceinline__ bool dev_value_apply(const float* v) {
 }
 
 // ------------------------------------------------------------------ jump kernel
-// grid (nseeds, ceil(nchunks / chunks_per_wg)); block kJumpThreads (8 waves).
+// grid (nseeds, ceil(nchunks / chunks_per_wg)); block kJumpThreads (16 waves).
 // LDS holds the seed's x[0..20560] (+ slack read by the last sliding window) at a
 // 3-word offset, so that y = x + 1 is 16-byte aligned.  Each wave evaluates the jump
-// of one chunk at a time: lane l < 52 owns window words w = 12l .. 12l+11 and sweeps
+// of one chunk at a time: lane l < 63 owns window words w = 10l .. 10l+9 and sweeps
 // the 19937 coefficients of c(t) = t^J mod phi four at a time, keeping
-// y[i + 12l .. i + 12l + 15] in a 16-register sliding window fed by one ds_read_b128
-// per step:  acc[j] ^= y[i + d + 12l + j] & -c[i + d]   (d = 0..3, j = 0..11).
-constexpr int kJumpLanes = 52;          // 52 lanes x 12 words = 624
+// y[i + 10l .. i + 10l + 15] in a 16-register sliding window fed by two ds_read_b64
+// per step:  acc[j] ^= y[i + d + 10l + j] & -c[i + d]   (d = 0..3, j = 0..9).
 constexpr int kJumpXOff = 3;            // x at word 3 -> y = x + 1 at word 4 (16 B aligned)
 constexpr int kJumpLdsWords = kJumpXOff + kJumpXLen + 64;  // + over-read slack of the last window
 
-__device__ __forceinline__ uint4 lds_b128(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
-
-// acc[j] ^= c0 * w[j] ^ c1 * w[j + 1] (j < 12) for the wave-uniform coefficient pair
-// two = c0 | c1 << 1.  Scalar branches skip a clear pair and pick the one-word or the
-// 3-input-xor body (v_bitop3), so a random polynomial costs 0.75 VALU ops per word and
-// coefficient pair instead of 2.  Inline asm: compiled from C the three bodies write
-// fresh registers and every merge copies the 12 accumulators back (v_mov x 12).
-__device__ __forceinline__ void jump_pair_step(uint32_t (&acc)[12], uint32_t w0, uint32_t w1, uint32_t w2,
-                                               uint32_t w3, uint32_t w4, uint32_t w5, uint32_t w6, uint32_t w7,
-                                               uint32_t w8, uint32_t w9, uint32_t w10, uint32_t w11, uint32_t w12,
-                                               uint32_t two) {
-  asm volatile(
-      "s_cmp_eq_u32 %[two], 0\n\t"
-      "s_cbranch_scc1 .Ljend%=\n\t"
-      "s_cmp_eq_u32 %[two], 3\n\t"
-      "s_cbranch_scc1 .Ljboth%=\n\t"
-      "s_cmp_eq_u32 %[two], 1\n\t"
-      "s_cbranch_scc1 .Ljone%=\n\t"
-      "v_xor_b32 %0, %0, %[w1]\n\tv_xor_b32 %1, %1, %[w2]\n\tv_xor_b32 %2, %2, %[w3]\n\t"
-      "v_xor_b32 %3, %3, %[w4]\n\tv_xor_b32 %4, %4, %[w5]\n\tv_xor_b32 %5, %5, %[w6]\n\t"
-      "v_xor_b32 %6, %6, %[w7]\n\tv_xor_b32 %7, %7, %[w8]\n\tv_xor_b32 %8, %8, %[w9]\n\t"
-      "v_xor_b32 %9, %9, %[w10]\n\tv_xor_b32 %10, %10, %[w11]\n\tv_xor_b32 %11, %11, %[w12]\n\t"
-      "s_branch .Ljend%=\n"
-      ".Ljone%=:\n\t"
-      "v_xor_b32 %0, %0, %[w0]\n\tv_xor_b32 %1, %1, %[w1]\n\tv_xor_b32 %2, %2, %[w2]\n\t"
-      "v_xor_b32 %3, %3, %[w3]\n\tv_xor_b32 %4, %4, %[w4]\n\tv_xor_b32 %5, %5, %[w5]\n\t"
-      "v_xor_b32 %6, %6, %[w6]\n\tv_xor_b32 %7, %7, %[w7]\n\tv_xor_b32 %8, %8, %[w8]\n\t"
-      "v_xor_b32 %9, %9, %[w9]\n\tv_xor_b32 %10, %10, %[w10]\n\tv_xor_b32 %11, %11, %[w11]\n\t"
-      "s_branch .Ljend%=\n"
-      ".Ljboth%=:\n\t"
-      "v_bitop3_b32 %0, %0, %[w0], %[w1] bitop3:0x96\n\tv_bitop3_b32 %1, %1, %[w1], %[w2] bitop3:0x96\n\t"
-      "v_bitop3_b32 %2, %2, %[w2], %[w3] bitop3:0x96\n\tv_bitop3_b32 %3, %3, %[w3], %[w4] bitop3:0x96\n\t"
-      "v_bitop3_b32 %4, %4, %[w4], %[w5] bitop3:0x96\n\tv_bitop3_b32 %5, %5, %[w5], %[w6] bitop3:0x96\n\t"
-      "v_bitop3_b32 %6, %6, %[w6], %[w7] bitop3:0x96\n\tv_bitop3_b32 %7, %7, %[w7], %[w8] bitop3:0x96\n\t"
-      "v_bitop3_b32 %8, %8, %[w8], %[w9] bitop3:0x96\n\tv_bitop3_b32 %9, %9, %[w9], %[w10] bitop3:0x96\n\t"
-      "v_bitop3_b32 %10, %10, %[w10], %[w11] bitop3:0x96\n\tv_bitop3_b32 %11, %11, %[w11], %[w12] bitop3:0x96\n"
-      ".Ljend%=:"
-      : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]),
-        "+v"(acc[7]), "+v"(acc[8]), "+v"(acc[9]), "+v"(acc[10]), "+v"(acc[11])
-      : [w0] "v"(w0), [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4), [w5] "v"(w5), [w6] "v"(w6),
-        [w7] "v"(w7), [w8] "v"(w8), [w9] "v"(w9), [w10] "v"(w10), [w11] "v"(w11), [w12] "v"(w12), [two] "s"(two)
-      : "scc");
-}
-
-// The same for 10 words per lane (FKS_JUMP_W10: 63 lanes x 10 words cover the 624 state
-// words, so 63 of 64 lanes work instead of 52): acc[j] ^= c0 * w[j] ^ c1 * w[j + 1], j < 10.
+// acc[j] ^= c0 * w[j] ^ c1 * w[j + 1] (j < 10) for the wave-uniform coefficient pair
+// two = c0 | c1 << 1 (63 lanes x 10 words cover the 624 state words).  Scalar branches
+// skip a clear pair and pick the one-word or the 3-input-xor body (v_bitop3), so a
+// random polynomial costs 0.75 VALU ops per word and coefficient pair instead of 2.
+// Inline asm: compiled from C the three bodies write fresh registers and every merge
+// copies the accumulators back.
 __device__ __forceinline__ void jump_pair_step10(uint32_t (&acc)[10], uint32_t w0, uint32_t w1, uint32_t w2,
                                                  uint32_t w3, uint32_t w4, uint32_t w5, uint32_t w6, uint32_t w7,
                                                  uint32_t w8, uint32_t w9, uint32_t w10, uint32_t two) {
@@ -492,11 +292,7 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
     __syncthreads();
   }
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-#if FKS_JUMP_W10
   constexpr int kW = 10, kLanes = 63;  // 63 lanes x 10 words (lane 62 keeps words 620..623)
-#else
-  constexpr int kW = 12, kLanes = kJumpLanes;
-#endif
   const uint32_t* yb = xs + 1 + kW * lane;  // y[kW lane]
   const int c0 = blockIdx.y * a.chunks_per_wg;
   const int c1 = min(c0 + a.chunks_per_wg, a.nchunks);
@@ -513,11 +309,7 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
         const uint64_t* poly = a.polys + (size_t)c * 312;  // wave-uniform: scalar loads
         uint32_t win[16];
         {
-#if FKS_JUMP_W10
           const uint4 q0 = lds_b64x2(yb), q1 = lds_b64x2(yb + 4), q2 = lds_b64x2(yb + 8), q3 = lds_b64x2(yb + 12);
-#else
-          const uint4 q0 = lds_b128(yb), q1 = lds_b128(yb + 4), q2 = lds_b128(yb + 8), q3 = lds_b128(yb + 12);
-#endif
           win[0] = q0.x; win[1] = q0.y; win[2] = q0.z; win[3] = q0.w;
           win[4] = q1.x; win[5] = q1.y; win[6] = q1.z; win[7] = q1.w;
           win[8] = q2.x; win[9] = q2.y; win[10] = q2.z; win[11] = q2.w;
@@ -532,11 +324,7 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
 #pragma unroll
           for (int q = 0; q < 16; q++) {
             // window = y[64 wd + 4q + kW lane + 0..15], stored rotated by 4q (mod 16)
-#if FKS_JUMP_W10
             const uint4 nx = lds_b64x2(yw + 4 * q + 16);
-#else
-            const uint4 nx = lds_b128(yw + 4 * q + 16);
-#endif
             const int rot = (4 * q) & 15;
             const uint32_t word = q < 8 ? lo : hi;
 #pragma unroll
@@ -546,18 +334,10 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
               // per word (v_bitop3), so a random polynomial costs 0.75 instead of 2
               // VALU ops per word and coefficient pair
               const uint32_t two = (word >> ((4 * q + d) & 31)) & 3u;
-#if FKS_JUMP_W10
               jump_pair_step10(acc, win[(rot + d) & 15], win[(rot + d + 1) & 15], win[(rot + d + 2) & 15],
                                win[(rot + d + 3) & 15], win[(rot + d + 4) & 15], win[(rot + d + 5) & 15],
                                win[(rot + d + 6) & 15], win[(rot + d + 7) & 15], win[(rot + d + 8) & 15],
                                win[(rot + d + 9) & 15], win[(rot + d + 10) & 15], two);
-#else
-              jump_pair_step(acc, win[(rot + d) & 15], win[(rot + d + 1) & 15], win[(rot + d + 2) & 15],
-                             win[(rot + d + 3) & 15], win[(rot + d + 4) & 15], win[(rot + d + 5) & 15],
-                             win[(rot + d + 6) & 15], win[(rot + d + 7) & 15], win[(rot + d + 8) & 15],
-                             win[(rot + d + 9) & 15], win[(rot + d + 10) & 15], win[(rot + d + 11) & 15],
-                             win[(rot + d + 12) & 15], two);
-#endif
             }
             win[(rot + 0) & 15] = nx.x;
             win[(rot + 1) & 15] = nx.y;
@@ -567,14 +347,9 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
         }
       }
       uint32_t* out = a.states + ((size_t)k * a.nchunks + c) * kMtN + kW * lane;
-#if FKS_JUMP_W10
 #pragma unroll
       for (int j = 0; j < kW; j += 2)
         if (kW * lane + j < kMtN) *reinterpret_cast<uint2*>(out + j) = make_uint2(acc[j], acc[j + 1]);
-#else
-#pragma unroll
-      for (int j = 0; j < kW; j += 4) *reinterpret_cast<uint4*>(out + j) = make_uint4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
-#endif
     }
   }
 }
@@ -754,9 +529,9 @@ __device__ __forceinline__ void twist_oop_reg(const TwistPlan& P, int src, int d
 __constant__ float c_tab_bf16[3 * 256];  // R | C | S, set once from fks::tables()
 
 // LDS: [R[256] f32 | (C,S)[256] f32x2 | windows (kMaxSeedsPerPass + 1) x 624 u32]
-// (FKS_RPAIR: R stored twice per 8-byte entry, same index scale as (C,S); measured 8 %
-// slower: the radius lookup moves twice the LDS bytes)
-constexpr int kLdsRBytes = FKS_RPAIR ? 256 * 8 : 256 * 4;
+// ((R,R) pairs at the (C,S) index scale measured 8 % slower: the radius lookup moves
+// twice the LDS bytes)
+constexpr int kLdsRBytes = 256 * 4;
 constexpr int kLdsTabBytes = kLdsRBytes + 256 * 8;
 constexpr int kLdsCsOff = kLdsRBytes;
 constexpr int kLdsStBytes = (kMaxSeedsPerPass + 1) * kMtN * 4;
@@ -790,7 +565,6 @@ __device__ __forceinline__ u32x2_t temper_pair_u8x8(u32x2_t y) {
   t = shl64<7>(y);
   y.x = __builtin_amdgcn_bitop3_b32(y.x, t.x, 0x9d2c5680u, kXorAnd);
   y.y = __builtin_amdgcn_bitop3_b32(y.y, t.y, 0x9d2c5680u, kXorAnd);
-#if FKS_TEMPER_FOLD
   // the third step y ^= (y << 15) & 0xefc60000 changes bits 17..31 only; of those the
   // index reads bits 18..25, where it adds y bits 3..10 under 0xF1 (= 0xefc60000 >> 18):
   // idx8 = ((y << 3) ^ (y >> 15) ^ (y & 0x788)) & 0x7F8 on the second step's y -- 6 ops
@@ -803,21 +577,12 @@ __device__ __forceinline__ u32x2_t temper_pair_u8x8(u32x2_t y) {
   o.x = __builtin_amdgcn_bitop3_b32(o.x, y.x, 0x788u, kXorAnd);
   o.y = __builtin_amdgcn_bitop3_b32(o.y, y.y, 0x788u, kXorAnd);
   return o;
-#else
-  t = shl64<15>(y);
-  y.x = __builtin_amdgcn_bitop3_b32(y.x, t.x, 0xefc60000u, kXorAnd);
-  y.y = __builtin_amdgcn_bitop3_b32(y.y, t.y, 0xefc60000u, kXorAnd);
-  const u32x2_t t1 = shl64<3>(y), t2 = shr64<15>(y);
-  u32x2_t o;
-  o.x = __builtin_amdgcn_bitop3_b32(t1.x, t2.x, 0x7F8u, kXorMask);
-  o.y = __builtin_amdgcn_bitop3_b32(t1.y, t2.y, 0x7F8u, kXorMask);
-  return o;
-#endif
 }
 
-// fp32 z pair from the two RAW words of a 16-block (FKS_F32_FAST): the same values as
-// z_pair_f32(mt_temper(r1), mt_temper(r2)) with fewer instructions, all exact rewrites
-// on this input domain (pinned by the golden fp32 streams):
+// fp32 z pair from the two RAW words of a 16-block: normal_fill_16_AVX2
+// (DistributionTemplates.h:88-106) with log256_ps / sincos256_ps (avx_mathfun.h:90-160,
+// 426-520), as oracle/fks_oracle.c restates it literally, with fewer instructions -- all
+// exact rewrites on this input domain (pinned by the golden fp32 streams):
 //   * both words tempered on the 64-bit pair (masks clear the bits one word shifts into
 //     the other; only the low 24 bits are kept);
 //   * theta = 2*pi*d2 >= +0, so sincos256_ps's sign extraction and abs are identities;
@@ -871,19 +636,10 @@ __device__ __forceinline__ void cephes_sincosf_nonneg(float x, float& s, float& 
 }
 
 // Correctly rounded sqrt of the radius input x = -2 log(u1), as _mm256_sqrt_ps: the
-// compiler's expansion, or (FKS_F32_RSQRT) v_sqrt_f32 -- NOT correctly rounded on this
-// domain by itself -- and one residual step to the neighbour, without the generic
-// denormal scaling (x is +-0 or >= 2^-23).  Either is checked on all 2^24 inputs against
-// the exact midpoint criterion (fks_device_selfcheck FKS_CHECK_SQRT_DOMAIN, a GPU test).
-__device__ __forceinline__ float radius_sqrt(float x) {
-  if (!FKS_F32_RSQRT) return sqrtf(x);  // the compiler's correctly rounded expansion
-  const float s = __builtin_amdgcn_sqrtf(x);
-  const float dn = __int_as_float(__float_as_int(s) - 1), up = __int_as_float(__float_as_int(s) + 1);
-  const float rdn = __fmaf_rn(-dn, s, x), rup = __fmaf_rn(-up, s, x);
-  float r = rdn <= 0.0f ? dn : s;
-  r = rup > 0.0f ? up : r;
-  return x > 0.0f ? r : x;
-}
+// compiler's correctly rounded expansion (a bare v_sqrt_f32 is NOT correctly rounded on
+// this domain), checked on all 2^24 inputs against the exact midpoint criterion
+// (fks_device_selfcheck FKS_CHECK_SQRT_DOMAIN, a GPU test).
+__device__ __forceinline__ float radius_sqrt(float x) { return sqrtf(x); }
 
 __device__ __forceinline__ void z_pair_f32_raw(uint32_t r1, uint32_t r2, float& z1, float& z2) {
   u32x2_t w;
@@ -903,30 +659,13 @@ __device__ __forceinline__ void z_pair_f32_raw(uint32_t r1, uint32_t r2, float& 
 // v_pk_fma_f32 (R*C is exact in f32: 8-bit x 8-bit significands; the +0 addend turns
 // -0 into +0 like normal_fill_16's "+ mean").  (R,R) pairs at LDS 0, (C,S) pairs at 2048.
 __device__ __forceinline__ f32x2_t z_pair_bf16_raw(uint32_t r1, uint32_t r2) {
-#if FKS_T64
   u32x2_t w;
   w.x = r1;
   w.y = r2;
   const u32x2_t ab = temper_pair_u8x8(w);
-  const uint32_t a8 = ab.x, b8 = ab.y;
-#else
-  const uint32_t a8 = mt_temper_u8x8(r1), b8 = mt_temper_u8x8(r2);
-#endif
-#if FKS_DIAG >= 3  // diagnostics: no table lookups (wrong values)
-  const f32x2_t rr = {__uint_as_float(a8 | 0x3f800000u), __uint_as_float(a8 | 0x3f800000u)};
-  const f32x2_t cs = {__uint_as_float(b8 | 0x3f000000u), __uint_as_float(b8 | 0x3e000000u)};
-#elif FKS_RPAIR == 2
-  const float r = lds_f32(a8);  // (R,R) entries read as one dword at the x8 index: no shift
+  const float r = lds_f32(ab.x >> 1);
   const f32x2_t rr = {r, r};
-  const f32x2_t cs = lds_f32x2(kLdsCsOff + b8);
-#elif FKS_RPAIR
-  const f32x2_t rr = lds_f32x2(a8);
-  const f32x2_t cs = lds_f32x2(kLdsCsOff + b8);
-#else
-  const float r = lds_f32(a8 >> 1);
-  const f32x2_t rr = {r, r};
-  const f32x2_t cs = lds_f32x2(kLdsCsOff + b8);
-#endif
+  const f32x2_t cs = lds_f32x2(kLdsCsOff + ab.y);
   const f32x2_t zero = {0.0f, 0.0f};
   return __builtin_elementwise_fma(rr, cs, zero);
 }
@@ -935,8 +674,7 @@ __device__ __forceinline__ f32x2_t z_pair_bf16_raw(uint32_t r1, uint32_t r2) {
 template <int DT>
 __device__ __forceinline__ void z_pair(const uint8_t* lds, uint32_t r1, uint32_t r2, float& z1, float& z2) {
   if constexpr (DT == FKS_F32) {
-    if (FKS_F32_FAST) z_pair_f32_raw(r1, r2, z1, z2);
-    else z_pair_f32(mt_temper(r1), mt_temper(r2), z1, z2);
+    z_pair_f32_raw(r1, r2, z1, z2);
   } else {
     // normal_fill_16<BFloat16>: z = bf16(R[a] * C[b]) * 1 + 0 (std, mean).  R*C is exact
     // in f32 (8-bit x 8-bit significands) and fma(R, C, +0) turns -0 into +0 like "+ mean".
@@ -975,7 +713,7 @@ __device__ __forceinline__ f32x2_t apply_pair(f32x2_t p, f32x2_t z, float g, flo
     f32x2_t t;
     if (MODE == kModeUpdateNoWd) {
       t = gz;
-    } else if (MODE == kModeUpdateWd0 && (DT != FKS_F32 || FKS_WD0_F32)) {
+    } else if (MODE == kModeUpdateWd0) {
       // wd = +-0: rnd(gz + rnd(wd*p)) == fma(wd, p, gz) (fks_internal.h)
       const f32x2_t ww = {wd, wd};
       t = __builtin_elementwise_fma(ww, p, gz);
@@ -1009,51 +747,21 @@ __device__ __forceinline__ f32x2_t z_pair2(const uint8_t* lds, uint32_t r1, uint
 
 // All seeds of the pass: every state-word read of the block is issued up front
 // (latency hidden behind the z math of earlier seeds), z for every seed next, then
-// the sequential per-element update chain in seed order.
+// the sequential per-element update chain in seed order.  (Staging every table index,
+// then every lookup, then the products measured no faster.)
 template <int DT, int MODE, int NS>
 __device__ __forceinline__ void pair_all(const uint8_t* lds, int st_off, const float* g, float lr, float wd,
                                          bool has_wd, float ps, float& p1, float& p2) {
   uint32_t r1[NS], r2[NS];
 #pragma unroll
   for (int k = 0; k < NS; k++) {
-#if FKS_DIAG == 4  // diagnostics: every lane reads the same (broadcast) words (wrong values)
-    const uint64_t w = lds_u64(kLdsTabBytes + k * kWinBytes);
-#else
     const uint64_t w = lds_u64(st_off + k * kWinBytes);  // (word j, word j+8), permuted window
-#endif
     r1[k] = (uint32_t)w;
     r2[k] = (uint32_t)(w >> 32);
   }
   f32x2_t z[NS];
-  if constexpr (DT == FKS_BF16 && FKS_STAGED) {
-    // staged: every table index first, then every lookup, then the products, so the
-    // LDS latency of the lookups overlaps the other seeds' tempering
-    uint32_t ia[NS], ib[NS];
 #pragma unroll
-    for (int k = 0; k < NS; k++) {
-      ia[k] = mt_temper_u8x8(r1[k]);
-      ib[k] = mt_temper_u8x8(r2[k]);
-    }
-    asm volatile("" ::: "memory");
-    f32x2_t rr[NS];
-    f32x2_t cs[NS];
-#pragma unroll
-    for (int k = 0; k < NS; k++) {
-      const float r = lds_f32(ia[k] >> 1);
-      rr[k].x = r;
-      rr[k].y = r;
-      cs[k] = lds_f32x2(kLdsCsOff + ib[k]);
-    }
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int k = 0; k < NS; k++) {
-      const f32x2_t zero = {0.0f, 0.0f};
-      z[k] = rnd2<DT>(__builtin_elementwise_fma(rr[k], cs[k], zero));
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < NS; k++) z[k] = z_pair2<DT>(lds, r1[k], r2[k]);
-  }
+  for (int k = 0; k < NS; k++) z[k] = z_pair2<DT>(lds, r1[k], r2[k]);
   f32x2_t p = {p1, p2};
 #pragma unroll
   for (int k = 0; k < NS; k++) p = apply_pair<DT, MODE>(p, z[k], g[k], lr, wd, has_wd, ps);
@@ -1082,7 +790,7 @@ __device__ __forceinline__ void pair_one(const uint8_t* lds, int st_off, int k, 
 constexpr int kDbThreads = kApplyThreads + 64;
 template <int DT, int MODE, bool FULL, bool DB = false>
 __global__ __launch_bounds__(DB ? kDbThreads : kApplyThreads,
-                             DB ? FKS_DB_MIN_WAVES : (kApplyWgPerCu * kApplyThreads + 255) / 256) void fks_apply_kernel(ApplyArgs a) {
+                             DB ? kDbMinWaves : (kApplyWgPerCu * kApplyThreads + 255) / 256) void fks_apply_kernel(ApplyArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
   // the lds_* accessors address LDS by offset from 0: the dynamic block must start there
@@ -1095,8 +803,7 @@ __global__ __launch_bounds__(DB ? kDbThreads : kApplyThreads,
   if constexpr (DT == FKS_BF16) {
     float2* tabCS = reinterpret_cast<float2*>(lds + kLdsCsOff);
     for (int i = tid; i < 256; i += kApplyThreads) {
-      if (FKS_RPAIR) reinterpret_cast<float2*>(lds)[i] = make_float2(c_tab_bf16[i], c_tab_bf16[i]);
-      else reinterpret_cast<float*>(lds)[i] = c_tab_bf16[i];
+      reinterpret_cast<float*>(lds)[i] = c_tab_bf16[i];
       tabCS[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
     }
   }
@@ -1204,7 +911,7 @@ __global__ __launch_bounds__(DB ? kDbThreads : kApplyThreads,
     if constexpr (DB) {
       buf = (int)((b - b0) & 1) * nseeds * kWinBytes;
       const int other = nseeds * kWinBytes - buf;
-      if (twister && b + 1 < b1 && (FKS_DIAG < 2 || FKS_DIAG == 5))  // block b+1, out of place
+      if (twister && b + 1 < b1)  // block b+1, out of place
         twist_oop(plan, buf + tw * kWinBytes, other + tw * kWinBytes);
       if (plan.wave == kWaves) {  // the twist-only wave
         __syncthreads();
@@ -1212,11 +919,11 @@ __global__ __launch_bounds__(DB ? kDbThreads : kApplyThreads,
       }
     } else {
       __syncthreads();  // every wave is done reading block b-1's words
-      if (FKS_DIAG < 2 || FKS_DIAG == 5) twist_all(plan, nseeds);  // the raw words of stream block b
+      twist_all(plan, nseeds);  // the raw words of stream block b
       __syncthreads();  // every window holds block b
     }
     const Slot nxt = fetch(b + 1 < b1 ? b + 1 : b);  // (the last block re-reads itself, unused)
-    if (FKS_DIAG != 1) {  // every lane: off lanes compute garbage into the sink
+    {  // every lane: off lanes compute garbage into the sink
       // even lane holds (p1, partner's p1), odd lane (partner's p2, p2)
       const uint32_t keep = odd ? ST::hi(sl.raw) : ST::lo(sl.raw);
       const uint32_t got = swap_adjacent(odd ? ST::lo(sl.raw) : ST::hi(sl.raw));
@@ -1233,32 +940,16 @@ __global__ __launch_bounds__(DB ? kDbThreads : kApplyThreads,
       const uint32_t b1v = ST::bits(p1), b2v = ST::bits(p2);
       const uint32_t back = swap_adjacent(odd ? b1v : b2v);  // even gets partner's p1, odd partner's p2
       const Pair out = odd ? ST::pack(back, b2v) : ST::pack(b1v, back);
-#if FKS_DIAG == 6
-      if (p1 == 1234.5f && p2 == -99.25f)
-#endif
       ST::store_pair(sl.addr, out);
     }
     if constexpr (DB) __syncthreads();  // block b+1 is twisted; block b's buffer is free
     return nxt;
   };
-  // Unrolled by two with the slots swapping roles, so the prefetched pair is consumed
-  // in the register it was loaded into: a loop-carried copy would need the load's
-  // vmcnt wait at the latch, and with in-order counters that also waits for the
-  // store just issued.
   Slot sa = fetch(b0);
   // a store after the first prefetch, so the loop is entered with the same pending
   // (load, store) shape as the back edge and the first wait can leave a store in flight
   *reinterpret_cast<volatile uint32_t*>(a.sink + 1) = 0u;
-  int64_t b = b0;
-#if FKS_UNROLL2
-  for (; b + 1 < b1; b += 2) {
-    const Slot sb = step(sa, b);
-    sa = step(sb, b + 1);
-  }
-  if (b < b1) step(sa, b);
-#else
-  for (; b < b1; b++) sa = step(sa, b);
-#endif
+  for (int64_t b = b0; b < b1; b++) sa = step(sa, b);
 }
 
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
@@ -1267,60 +958,14 @@ __device__ __forceinline__ u32x4_t lds_u4(uint32_t off) { return *(const lds_u4_
 __device__ __forceinline__ void lds_st4(uint32_t off, u32x4_t v) { *(lds_u4_t*)(size_t)off = v; }
 
 // ------------------------------------------------------------------ small-K kernel v2
-// Table layouts of the small-K kernel's bf16 z (FKS_SM2_TAB): 0 = R f32[256] | (C,S)
-// f32x2[256] (one ds_read_b64 per pair, as the other kernels); 1 = R | C | S as three
-// f32[256] tables read at one x4 index (C and S with one ds_read2st64_b32); 2 = R |
-// (C,S) packed as two bf16 in one dword (ds_read_b32 + two unpack ops).  A random
-// 8-bit-indexed ds_read_b64 costs ~2.7x a ds_read_b32 in LDS cycles (tools/ubench/issue2),
-// and the small-K kernel shares its LDS pipe between 32 waves per CU.
-// x4-scaled folded tempering index of a word pair: ((y << 2) ^ (y >> 16)) & 0x3FC ^
-// ((y >> 1) & 0x3C4) on the second step's y (tests/test_temper_fold.py)
-__device__ __forceinline__ u32x2_t temper_pair_u8x4(u32x2_t y) {
-  u32x2_t t = shr64<11>(y);
-  y.x = __builtin_amdgcn_bitop3_b32(y.x, t.x, 0x001FFFFFu, kXorAnd);
-  y.y ^= t.y;
-  t = shl64<7>(y);
-  y.x = __builtin_amdgcn_bitop3_b32(y.x, t.x, 0x9d2c5680u, kXorAnd);
-  y.y = __builtin_amdgcn_bitop3_b32(y.y, t.y, 0x9d2c5680u, kXorAnd);
-  const u32x2_t t1 = shl64<2>(y), t2 = shr64<16>(y), t3 = shr64<1>(y);
-  u32x2_t o;
-  o.x = __builtin_amdgcn_bitop3_b32(t1.x, t2.x, 0x3FCu, kXorMask);
-  o.y = __builtin_amdgcn_bitop3_b32(t1.y, t2.y, 0x3FCu, kXorMask);
-  o.x = __builtin_amdgcn_bitop3_b32(o.x, t3.x, 0x3C4u, kXorAnd);
-  o.y = __builtin_amdgcn_bitop3_b32(o.y, t3.y, 0x3C4u, kXorAnd);
-  return o;
-}
-
+// (Other bf16 table layouts for the small-K kernel -- R|C|S f32, (C,S) packed as bf16 --
+// measured within noise or slower: profiles/r02_smallk_ab.log.)
 // bf16 z pair from the two table byte offsets (x8) of temper_pair_u8x8: the lookups and
 // the rounding of z_pair_bf16_raw (default table layout)
 __device__ __forceinline__ f32x2_t z_bf16_idx8(uint32_t a8, uint32_t b8) {
   const float r = lds_f32(a8 >> 1);
   const f32x2_t rr = {r, r}, zero = {0.0f, 0.0f};
   return rnd2<FKS_BF16>(__builtin_elementwise_fma(rr, lds_f32x2(kLdsCsOff + b8), zero));
-}
-
-template <int DT>
-__device__ __forceinline__ f32x2_t z_pair_sm2(const uint8_t* lds, uint32_t r1, uint32_t r2) {
-  if constexpr (DT != FKS_BF16 || FKS_SM2_TAB == 0) {
-    return z_pair2<DT>(lds, r1, r2);
-  } else {
-    u32x2_t w;
-    w.x = r1;
-    w.y = r2;
-    const u32x2_t ab = temper_pair_u8x4(w);
-    const float r = lds_f32(ab.x);
-    f32x2_t cs;
-    if constexpr (FKS_SM2_TAB == 1) {
-      cs.x = lds_f32(1024 + ab.y);
-      cs.y = lds_f32(2048 + ab.y);
-    } else {
-      const uint32_t v = lds_u32(1024 + ab.y);
-      cs.x = __uint_as_float(v << 16);
-      cs.y = __uint_as_float(v & 0xffff0000u);
-    }
-    const f32x2_t rr = {r, r}, zero = {0.0f, 0.0f};
-    return rnd2<DT>(__builtin_elementwise_fma(rr, cs, zero));
-  }
 }
 
 // fks_small2_kernel<DT, MODE>: passes of <= kSmallK seeds over fast segments (the ZO
@@ -1359,9 +1004,8 @@ __device__ __forceinline__ float rflf(float v) { return __uint_as_float(rfl(__fl
 constexpr int kZidxPerBlock = kSm2ZidxPerBlock;  // u32 per block
 static_assert(kSm2ZidxPerBlock == kSm2PairLanes, "one z-index word per pair lane");
 template <int DT, int MODE, int ZM = 0>
-__global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_kernel(ApplyArgs a) {
-  static_assert(ZM == 0 || (ZM == 1 && DT == FKS_BF16 && FKS_SM2_TAB == 0 && !FKS_RPAIR),
-                "z-index store: bf16, default tables");
+__global__ __launch_bounds__(kSm2Threads, kSm2MinWaves) void fks_small2_kernel(ApplyArgs a) {
+  static_assert(ZM == 0 || (ZM == 1 && DT == FKS_BF16), "z-index store: bf16");
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
   if ((uint32_t)(size_t)(lds_u32_t*)lds32 != 0u) __builtin_trap();
@@ -1372,20 +1016,9 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
   const int nblk = (int)(a.chunk_block[c + 1] - b0);  // host: a chunk is far below 2^31 blocks
 
   if constexpr (DT == FKS_BF16) {
-    for (int i = tid; i < 256; i += (int)blockDim.x) {  // (a replay launches 3 waves)
-      if (FKS_SM2_TAB == 1) {
-        reinterpret_cast<float*>(lds)[i] = c_tab_bf16[i];
-        reinterpret_cast<float*>(lds + 1024)[i] = c_tab_bf16[256 + i];
-        reinterpret_cast<float*>(lds + 2048)[i] = c_tab_bf16[512 + i];
-      } else if (FKS_SM2_TAB == 2) {  // C, S are bf16-exact: (C bits >> 16) | (S bits & 0xffff0000)
-        reinterpret_cast<float*>(lds)[i] = c_tab_bf16[i];
-        reinterpret_cast<uint32_t*>(lds + 1024)[i] =
-            (__float_as_uint(c_tab_bf16[256 + i]) >> 16) | (__float_as_uint(c_tab_bf16[512 + i]) & 0xffff0000u);
-      } else {
-        if (FKS_RPAIR) reinterpret_cast<float2*>(lds)[i] = make_float2(c_tab_bf16[i], c_tab_bf16[i]);
-        else reinterpret_cast<float*>(lds)[i] = c_tab_bf16[i];
-        reinterpret_cast<float2*>(lds + kLdsCsOff)[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
-      }
+    for (int i = tid; i < 256; i += (int)blockDim.x) {
+      reinterpret_cast<float*>(lds)[i] = c_tab_bf16[i];
+      reinterpret_cast<float2*>(lds + kLdsCsOff)[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
     }
   }
   // the chunk-start windows go to buffer 1, twisted into buffer 0 for block b0
@@ -1404,18 +1037,15 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
       constexpr int D = decltype(dst_c)::value;
 #pragma unroll
       for (int k = 0; k < kSmallK; k++)
-        if (k < nseeds) {
-          if (FKS_SM2_TWREG) twist_oop_reg(plan, (2 * k + 1 - D) * kWinBytes, (2 * k + D) * kWinBytes);
-          else twist_oop(plan, (2 * k + 1 - D) * kWinBytes, (2 * k + D) * kWinBytes);
-        }
+        if (k < nseeds) twist_oop_reg(plan, (2 * k + 1 - D) * kWinBytes, (2 * k + D) * kWinBytes);
     };
     if (nblk > 0) twist_into(std::integral_constant<int, 0>{});
     __syncthreads();
     for (int t = 0; t < nblk; t += 2) {
-      if (t + 1 < nblk && FKS_DIAG != 2) twist_into(std::integral_constant<int, 1>{});
+      if (t + 1 < nblk) twist_into(std::integral_constant<int, 1>{});
       __syncthreads();  // block t+1 is in buffer 1; block t's buffer 0 is free
       if (t + 1 >= nblk) break;
-      if (t + 2 < nblk && FKS_DIAG != 2) twist_into(std::integral_constant<int, 0>{});
+      if (t + 2 < nblk) twist_into(std::integral_constant<int, 0>{});
       __syncthreads();
     }
     return;
@@ -1518,8 +1148,8 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
           zB = z_bf16_idx8(zcd.x, zcd.y);
         } else {
           const u32x4_t w = lds_u4(st_off + (uint32_t)((2 * k + B) * kWinBytes));
-          zA = z_pair_sm2<DT>(lds, w.x, w.y);
-          zB = z_pair_sm2<DT>(lds, w.z, w.w);
+          zA = z_pair2<DT>(lds, w.x, w.y);
+          zB = z_pair2<DT>(lds, w.z, w.w);
         }
         pA = apply_pair<DT, MODE>(pA, zA, gk[k], lr, wd, wdf, ps, upd);
         pB = apply_pair<DT, MODE>(pB, zB, gk[k], lr, wd, wdf, ps, upd);
@@ -1548,7 +1178,7 @@ __global__ __launch_bounds__(kSm2Threads, FKS_SM2_MIN_WAVES) void fks_small2_ker
       a.zidx[((size_t)(b0 + t - a.zlo)) * kZidxPerBlock + q] =
           (zab.x >> 3) | (zab.y << 5) | (zcd.x << 13) | (zcd.y << 21);
     }
-    if (FKS_DIAG != 1) {
+    {
       if (sl.fast) {
         run(buf_c, sl.r0, sl.r1, u_lr, u_wd, u_wdf, u_ps);
         ST::store_pair(sl.base + joff, sl.r0);
@@ -1625,13 +1255,12 @@ __global__ __launch_bounds__(kZrThreads) void fks_zreplay_kernel(ApplyArgs a) {
     reinterpret_cast<float*>(lds32)[512 + i] = c_tab_bf16[512 + i];
   }
   __syncthreads();
-  // FKS_ZR_GRID: tiles of the whole call are dealt round-robin over the workgroups, so the
-  // workgroups in flight stream neighbouring addresses (few pages live at a time, as a
-  // grid-stride elementwise kernel); else workgroup c walks chunk c's tiles
-  const int64_t P0 = (int64_t)kMtN * a.chunk_block[0], P1 = (int64_t)kMtN * a.chunk_block[a.nchunks];
-  const int64_t p0 = FKS_ZR_GRID ? P0 + (int64_t)c * kZrTile : (int64_t)kMtN * a.chunk_block[c];
-  const int64_t p1 = FKS_ZR_GRID ? P1 : (int64_t)kMtN * a.chunk_block[c + 1];
-  const int64_t tstep = FKS_ZR_GRID ? (int64_t)gridDim.x * kZrTile : kZrTile;
+  // tiles of the whole call are dealt round-robin over the workgroups, so the workgroups
+  // in flight stream neighbouring addresses (few pages live at a time, as a grid-stride
+  // elementwise kernel; one chunk per workgroup measured slower)
+  const int64_t p0 = (int64_t)kMtN * a.chunk_block[0] + (int64_t)c * kZrTile;
+  const int64_t p1 = (int64_t)kMtN * a.chunk_block[a.nchunks];
+  const int64_t tstep = (int64_t)gridDim.x * kZrTile;
   const int64_t zbase = (int64_t)kMtN * a.zlo;
   const uint64_t zb = (uint64_t)(uintptr_t)a.zidx;
   float g = rflf(a.g[0]);
@@ -1673,7 +1302,7 @@ __global__ __launch_bounds__(kZrThreads) void fks_zreplay_kernel(ApplyArgs a) {
     return out;
   };
   const u32x4_t zero4 = {0u, 0u, 0u, 0u};
-  // FKS_ZR_UNROLL tiles per iteration: every tile's index records and parameters are
+  // kZrUnroll tiles per iteration: every tile's index records and parameters are
   // loaded before the first is computed, so a wave keeps that many tiles in flight (a
   // straddling tile loads its parameters when it runs)
   struct ZSlot { int64_t t0; uint64_t base; float lr, wd, ps; int cur; bool fast, wdf; u32x4_t rec, pv; };
@@ -1727,11 +1356,7 @@ __global__ __launch_bounds__(kZrThreads) void fks_zreplay_kernel(ApplyArgs a) {
     const int64_t pos = z.t0 + 8 * (int64_t)tid;
     if (pos >= p1) return;
     if (z.fast) {
-#if FKS_DIAG == 8  // diagnostics: the replay's memory traffic without its arithmetic (wrong values)
-      gstore4(z.base + 16u * (uint32_t)tid, z.pv ^ z.rec);
-#else
       gstore4(z.base + 16u * (uint32_t)tid, chain(z.pv, z.rec, z.lr, z.wd, z.wdf, z.ps));
-#endif
     } else {
       int cc = z.cur;
       bool in = false;
@@ -1748,7 +1373,7 @@ __global__ __launch_bounds__(kZrThreads) void fks_zreplay_kernel(ApplyArgs a) {
       }
     }
   };
-  constexpr int kU = FKS_ZR_UNROLL;
+  constexpr int kU = kZrUnroll;
   for (int64_t t0 = p0; t0 < p1; t0 += kU * tstep) {
     ZSlot z[kU];
 #pragma unroll
@@ -1762,39 +1387,41 @@ __global__ __launch_bounds__(kZrThreads) void fks_zreplay_kernel(ApplyArgs a) {
 // fks_apply_bs_kernel<MODE>: the bf16 fast segments of a reconstruct, 32 seeds per
 // pass, generator state BIT-SLICED (fks_bitslice.h).  One workgroup per CU, two
 // independent halves (chunks 2w and 2w+1 of the stream) sharing the LDS tables:
-//   * waves 0..4 of a half: thread q < 312 owns Box-Muller pair q of every block, as in
-//     fks_apply_kernel; per block it reads state rows j1 and j1+8 (32 planes each),
-//     tempers their low bytes (temper_low8), transposes them to one byte per seed
-//     (transpose8), and runs the 32-seed update chain of its two parameters in order;
-//   * wave 5 of a half twists the half's state in place, block b -> b+1, while the
-//     pair waves run block b's chain: 10 rounds of 64 rows, all reads of a round
-//     before its writes (one wave: LDS operations complete in order, so no barrier).
-// Per block: barrier (state holds block b) -> pair waves read + temper their rows ->
-// barrier (rows consumed) -> twist || chain.
-// LDS: [R f32 x 256 | (C,S) f32x2 x 256 | state half 0 | state half 1]; a half's state
-// is 8 CHUNK arrays (planes 4q..4q+3 of all 624 rows, 16 B per row): consecutive rows
-// are consecutive 16 B, so the twist wave's row reads and writes are bank-conflict
-// free; the pair waves read row j1 first where (q >> 4) is even and row j1+8 first
-// where it is odd, which makes every 16-lane ds_read_b128 group hit 16 distinct rows
-// mod 16 (conflict free as well).
+//   * waves 0..4 of a half (pair waves): thread q < 312 owns Box-Muller pair q of every
+//     block; per block it reads state rows j1 and j1+8 (32 planes each), tempers their
+//     low bytes (temper_low8), transposes them to one byte per seed (transpose8), and
+//     runs the 32-seed update chain of its two parameters in order;
+//   * wave 5 of a half (twist wave) twists the half's state in place, block b -> b+1,
+//     while the pair waves run block b's chain: 10 rounds of 64 rows, all reads of a
+//     round before its writes (one wave: LDS operations complete in order).
+// Per block: barrier 1 (every pair wave holds block b's rows) -> twist || chain ->
+// barrier 2 (block b+1 is in place) -> the pair waves read + temper their rows.
+// (Replacing the two barriers by LDS flags -- each pair wave reading its rows as soon as
+// the twist rounds that write them are published, the halves drifting apart -- measured
+// 1-10 % SLOWER, and reading the next rows 4-16 seeds before the chain ends no faster:
+// profiles/r03b_ab_flags.log, r03d_ab_prefetch.log.)
+// LDS: [R f32 x 256 | (C,S) table | state half 0 | state half 1]; a half's state is 8
+// CHUNK arrays (planes 4q..4q+3 of all 624 rows, 16 B per row): consecutive rows are
+// consecutive 16 B, so the twist wave's row reads and writes are bank-conflict free; the
+// pair waves read row j1 first where (q >> 4) is even and row j1+8 first where it is
+// odd, which makes every 16-lane ds_read_b128 group hit 16 distinct rows mod 16.
 constexpr int kBsChunkBytes = kMtN * 16;               // 9,984
 constexpr int kBsStateBytes = 8 * kBsChunkBytes;       // 79,872
-// (C,S): f32 pairs (8 B, ds_read_b64) or, FKS_BS_CSPACK, the two bf16 values packed in one
-// dword (4 B, ds_read_b32): a random 8-bit-indexed ds_read_b64 measured 17.4 CU-cycles per
-// wave-instruction against 6.5 for ds_read_b32 (tools/ubench/issue2.hip), for two unpack ops
-constexpr int kBsCsBytes = 8;                          // room for either layout
-// FKS_BS_PLANAR: the S table 1024 B after C (one ds_read2st64_b32 for both) or, PLANAR 2,
-// 1028 B after (no read2 form reaches it: two ds_read_b32)
-constexpr int kBsSTabOff = FKS_BS_PLANAR == 2 ? 2052 : 2048;
-constexpr int kBsTabBytes = FKS_BS_PLANAR == 2 ? 3088 : 256 * 4 + 256 * kBsCsBytes;  // 3,072
+// (C,S): f32 pairs (8 B, ds_read_b64) or the two bf16 values packed in one dword (4 B,
+// ds_read_b32 + two unpack ops) for the chains without the weight-decay roundings
+// (kModeUpdateWd0 / NoWd: 3.84 vs 4.03 ms per launch, profiles/r02g_ab_wd0.log; a random
+// 8-bit-indexed ds_read_b64 costs 17.4 CU-cycles per wave-instruction against 6.5 for
+// ds_read_b32, tools/ubench/issue2.hip).  Planar C|S tables read by ds_read2st64_b32 or
+// two ds_read_b32 measured +19 % / +24 % (profiles/r02j_ab_planar.log, r02u_ab_planar2.log).
+constexpr int kBsCsBytes = 8;
+constexpr int kBsTabBytes = 256 * 4 + 256 * kBsCsBytes;  // 3,072
 template <int MODE>
 constexpr bool bs_cspack() {
-  return !FKS_BS_PLANAR &&
-         (FKS_BS_CSPACK == 1 || (FKS_BS_CSPACK == 2 && (MODE == kModeUpdateWd0 || MODE == kModeUpdateNoWd)));
+  return MODE == kModeUpdateWd0 || MODE == kModeUpdateNoWd;
 }
 constexpr int kBsLdsBytes = kBsTabBytes + 2 * kBsStateBytes;  // 162,816 <= 163,840
 static_assert(kBsLdsBytes <= 163840, "slice kernel LDS");
-
+constexpr int kBsRounds = 10;                          // twist rounds of 64 rows per block
 
 // the 32 planes of row i (row byte address ra = state base + 16 i)
 __device__ __forceinline__ void bs_load_row(uint32_t ra, uint32_t (&x)[32]) {
@@ -1840,31 +1467,19 @@ __device__ __forceinline__ void bs_twist_block(uint32_t sbase, int lane) {
   bs_load_row(av, V);
   bs_load_row(am, M);
 #pragma unroll
-  for (int r = 0; r < 10; r++) {
+  for (int r = 0; r < kBsRounds; r++) {
     uint32_t Vn[32], Mn[32];
-    if (r + 1 < 10) {
+    if (r + 1 < kBsRounds) {
       uint32_t avn, amn;
       bs_round_rows(sbase, r + 1, lane, avn, amn);
-#if FKS_BS_DIAG == 7  // diagnostics: the twist loads nothing after round 0 (wrong values)
-#pragma unroll
-      for (int b = 0; b < 32; b++) {
-        Vn[b] = V[b] ^ avn;
-        Mn[b] = M[b] ^ amn;
-      }
-#else
       bs_load_row(avn, Vn);
       bs_load_row(amn, Mn);
-#endif
     }
     const uint32_t u31 = (uint32_t)__builtin_amdgcn_update_dpp((int)prev63, (int)V[31], 0x138, 0xF, 0xF, false);
     prev63 = (uint32_t)__builtin_amdgcn_readlane((int)V[31], 63);
     bs::twist_row_inplace(V, M, u31);  // M now holds the new row i
-#if FKS_BS_DIAG == 6  // diagnostics: the twist stores nothing (wrong values)
-    if (r == 9 && 64 * r + lane < 0) bs_store_row(sbase + 16u * (uint32_t)(64 * r + lane), M);
-#else
-    if (r < 9 || 64 * r + lane < kMtN) bs_store_row(sbase + 16u * (uint32_t)(64 * r + lane), M);
-#endif
-    if (r + 1 < 10) {
+    if (r < kBsRounds - 1 || 64 * r + lane < kMtN) bs_store_row(sbase + 16u * (uint32_t)(64 * r + lane), M);
+    if (r + 1 < kBsRounds) {
 #pragma unroll
       for (int b = 0; b < 32; b++) {
         V[b] = Vn[b];
@@ -1891,18 +1506,12 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   if ((uint32_t)(size_t)(lds_u32_t*)lds32 != 0u) __builtin_trap();
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-#if FKS_BS_ROLEMAP == 1
-  // waves w, w+4, w+8 share a SIMD (profiles/r02f_simdmap.log): the two twist waves at
-  // w = 5 (half 0) and w = 9 (half 1) share SIMD 1 with one pair wave
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int half = w >= 6 ? 1 : 0;
-  const int hw = w < 5 ? w : (w == 5 || w == 9 ? 5 : (w < 9 ? w - 6 : w - 7));
-  const int ht = hw * 64 + lane;
-#else
   const int half = __builtin_amdgcn_readfirstlane(tid >= kBsHalfThreads ? 1 : 0);
   const int ht = tid - half * kBsHalfThreads;
-  const int hw = __builtin_amdgcn_readfirstlane(ht >> 6);  // 0..4 pair waves, 5 twist wave
-#endif
+  // waves 0..4 of a half pair waves, 5 the twist wave: waves w, w+4, w+8 share a SIMD
+  // (profiles/r02f_simdmap.log), so the twist waves 5 and 11 sit on SIMDs 1 and 3
+  // (both on one SIMD measured +5 %, profiles/r02i_ab_rolemap.log)
+  const int hw = __builtin_amdgcn_readfirstlane(ht >> 6);
   const int c = kBsChunksPerWg * (int)blockIdx.x + half;
   const int nseeds = FULL ? kBsSeeds : a.nseeds;
   const int64_t b0 = a.chunk_block[c], b1 = a.chunk_block[c + 1];
@@ -1915,10 +1524,7 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
 
   for (int i = tid; i < 256; i += kBsThreads) {
     reinterpret_cast<float*>((uint8_t*)lds32)[i] = c_tab_bf16[i];
-    if (FKS_BS_PLANAR) {
-      reinterpret_cast<float*>((uint8_t*)lds32 + 1024)[i] = c_tab_bf16[256 + i];
-      reinterpret_cast<float*>((uint8_t*)lds32 + kBsSTabOff)[i] = c_tab_bf16[512 + i];
-    } else if (bs_cspack<MODE>())  // C in the low half, S in the high half (both exact bf16 values)
+    if (bs_cspack<MODE>())  // C in the low half, S in the high half (both exact bf16 values)
       reinterpret_cast<uint32_t*>((uint8_t*)lds32 + 1024)[i] =
           (__float_as_uint(c_tab_bf16[256 + i]) >> 16) | (__float_as_uint(c_tab_bf16[512 + i]) & 0xffff0000u);
     else
@@ -1937,22 +1543,19 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   // sequence (s_barrier is workgroup-wide whatever the program counter), so the
   // twist's 4 x 32 row registers are never live together with the pair state.
   if (hw == 5) {
-    // (FKS_BS_PRIO: the twist wave issuing first measured 5 % slower)
-    if (FKS_BS_PRIO) __builtin_amdgcn_s_setprio(FKS_BS_PRIO);
     if (mynb > 0) bs_twist_block(sbase, lane);  // -> block b0
     __syncthreads();                              // state holds block b0
     for (int64_t t = 0; t < nb; t++) {
-      if (FKS_BS_DIAG != 5) __syncthreads();      // every pair wave holds its rows of block b
-      if (t + 1 < mynb && FKS_BS_DIAG != 1) bs_twist_block(sbase, lane);  // -> block b + 1
-      if (FKS_BS_DIAG != 5) __syncthreads();
+      __syncthreads();                            // every pair wave holds its rows of block b
+      if (t + 1 < mynb) bs_twist_block(sbase, lane);  // -> block b + 1
+      __syncthreads();
     }
     return;
   }
 
   // pair lanes (waves 0..4 of the half)
-  const bool pair_wave = true;
   const int q = ht < kMtN / 2 ? ht : kMtN / 2 - 1;
-  const bool lane_on = pair_wave && ht < kMtN / 2;
+  const bool lane_on = ht < kMtN / 2;
   const int j1 = 16 * (q >> 3) + (q & 7);
   const bool flip = ((q >> 4) & 1) != 0;
   const uint32_t ra_first = sbase + 16u * (uint32_t)(flip ? j1 + 8 : j1);
@@ -1961,10 +1564,9 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   float gk[kBsSeeds];
 #pragma unroll
   for (int k = 0; k < kBsSeeds; k++) gk[k] = a.g[k];
-  // The pair waves set the block time and the twist wave has slack: on the two SIMDs
-  // that hold a twist wave, the pair waves issue first (measured 6 % faster per launch;
-  // the twist wave issuing first instead is 5 % slower).
-  if (FKS_BS_PAIR_PRIO) __builtin_amdgcn_s_setprio(FKS_BS_PAIR_PRIO);
+  // the pair waves issue first on the two SIMDs that also hold a twist wave (measured
+  // 6 % faster per launch; the twist wave first instead: 5 % slower)
+  __builtin_amdgcn_s_setprio(1);
 
   // the lane's current segment (positions only grow)
   int cur;
@@ -1995,7 +1597,7 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): see fks_apply_kernel
   };
-  if (pair_wave) load_seg();
+  load_seg();
 
   const bool odd = (tid & 1) != 0;
   using ST = Traits<MODE == kModeDelta ? FKS_F32 : FKS_BF16>;
@@ -2019,7 +1621,10 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   // rows j1 and j1 + 8 of the state -> the lane's tempered radius / angle bytes, 8 planes
   // each (transposed to one byte per seed right before use)
   uint32_t oa[8], ob[8];
-  auto temper_rows = [&](const uint32_t (&x1)[32], const uint32_t (&x2)[32]) {
+  auto read_rows = [&]() {
+    uint32_t x1[32], x2[32];
+    bs_load_row(ra_first, x1);  // (the last block re-reads rows it does not use)
+    bs_load_row(ra_second, x2);
     uint32_t o1[8], o2[8];
     bs::temper_low8(x1, o1);
     bs::temper_low8(x2, o2);
@@ -2032,109 +1637,58 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   // seed k's table lookups (R[a], (C,S)[b]) and its step of the update chain
   auto lookup = [&](int k, f32x2_t& rr, f32x2_t& cs) {
     const uint32_t ia = bs_index<2>(oa[k & 7], k >> 3);
-    const uint32_t ib = bs_index<(bs_cspack<MODE>() || FKS_BS_PLANAR) ? 2 : 3>(ob[k & 7], k >> 3);
-#if FKS_BS_DIAG == 3  // diagnostics: no table lookups (wrong values)
-    rr = f32x2_t{__uint_as_float(ia | 0x3f800000u), __uint_as_float(ia | 0x3f800000u)};
-    cs = f32x2_t{__uint_as_float(ib | 0x3f000000u), __uint_as_float(ib | 0x3e000000u)};
-#else
+    const uint32_t ib = bs_index<bs_cspack<MODE>() ? 2 : 3>(ob[k & 7], k >> 3);
     const float r = lds_f32(ia);
     rr = f32x2_t{r, r};
-    if (FKS_BS_PLANAR) {  // C[b] and S[b] 1024 B apart: one ds_read2st64_b32
-      cs = f32x2_t{lds_f32(1024u + ib), lds_f32((uint32_t)kBsSTabOff + ib)};
-    } else if (bs_cspack<MODE>()) {
+    if (bs_cspack<MODE>()) {
       const uint32_t w = lds_u32((int)(1024u + ib));
       cs = f32x2_t{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
     } else {
       cs = lds_f32x2(1024u + ib);
     }
-#endif
   };
   auto chain = [&](int k, f32x2_t p, f32x2_t rr, f32x2_t cs) -> f32x2_t {
     const f32x2_t zero = {0.0f, 0.0f};
     const f32x2_t z = rnd2<FKS_BF16>(__builtin_elementwise_fma(rr, cs, zero));
     return apply_pair<FKS_BF16, MODE>(p, z, gk[k], sl.lr, sl.wd, sl.wdf != 0, 0.0f);
   };
-  if (mynb > 0) {
-    uint32_t x1[32], x2[32];
-    bs_load_row(ra_first, x1);
-    bs_load_row(ra_second, x2);
-    temper_rows(x1, x2);
-  }
+  if (mynb > 0) read_rows();
 
-  // Per block: barrier 1 (every pair wave holds block b's rows; the twist wave starts
-  // block b+1) -> the first kHead seeds -> barrier 2 (block b+1 is in place) -> the last
-  // kTail seeds' lookups, then block b+1's row reads, then the tail of the chain: the
-  // row-read latency hides behind this block's last seeds instead of idling the VALU.
-  constexpr int kTail = FKS_BS_TAIL, kHead = kBsSeeds - kTail;
   for (int64_t t = 0; t < nb; t++) {
     const bool act = t < mynb;  // half-uniform
     const int64_t b = b0 + t;
-    if (FKS_BS_DIAG != 5) __syncthreads();  // barrier 1
-    f32x2_t p = {0.0f, 0.0f};
-    Slot nxt = sl;
-    if (act && FKS_BS_DIAG != 2) {
-      nxt = fetch(b + 1 < b1 ? b + 1 : b);
+    __syncthreads();  // barrier 1: every pair wave holds block b's rows; the twist starts block b+1
+    if (act) {
+      const Slot nxt = fetch(b + 1 < b1 ? b + 1 : b);
       bs::transpose8(oa);
       bs::transpose8(ob);
-      const uint32_t keep = odd ? ST::hi(sl.raw) : ST::lo(sl.raw);
-      const uint32_t got = swap_adjacent(odd ? ST::lo(sl.raw) : ST::hi(sl.raw));
-      p.x = ST::cvt(odd ? got : keep);
-      p.y = ST::cvt(odd ? keep : got);
-      if (FKS_BS_LA > 0) {
-        // software-pipelined lookups: seed k + LA's table reads are issued right after
-        // seed k's chain, so each chain step waits on reads issued LA steps earlier (the
-        // compiler left on its own hoists them one seed only, and every step then waits
-        // for its own bank-conflicted reads)
-        constexpr int LA = FKS_BS_LA > 0 ? FKS_BS_LA : 1;
-        f32x2_t lrr[LA], lcs[LA];
-#pragma unroll
-        for (int k = 0; k < LA && k < kHead; k++)
-          if (FULL || k < nseeds) lookup(k, lrr[k], lcs[k]);
-        FKS_BS_SCHED_FENCE();
-#pragma unroll
-        for (int k = 0; k < kHead; k++) {
-          if (FULL || k < nseeds) p = chain(k, p, lrr[k % LA], lcs[k % LA]);
-          FKS_BS_SCHED_FENCE();
-          if (k + LA < kHead && (FULL || k + LA < nseeds)) lookup(k + LA, lrr[k % LA], lcs[k % LA]);
-          FKS_BS_SCHED_FENCE();
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < kHead; k++) {
-          if (FULL || k < nseeds) {
-            f32x2_t rr, cs;
-            lookup(k, rr, cs);
-            p = chain(k, p, rr, cs);
-          }
-          // the lookups of one byte column (8 seeds) at a time: hoisting all 64 table
-          // reads ahead of the chain would spill
-          if (FKS_BS_FENCE && (k % FKS_BS_FENCE) == FKS_BS_FENCE - 1) asm volatile("" ::: "memory");
-        }
+      f32x2_t p;
+      {
+        const uint32_t keep = odd ? ST::hi(sl.raw) : ST::lo(sl.raw);
+        const uint32_t got = swap_adjacent(odd ? ST::lo(sl.raw) : ST::hi(sl.raw));
+        p.x = ST::cvt(odd ? got : keep);
+        p.y = ST::cvt(odd ? keep : got);
       }
-    }
-    if (FKS_BS_DIAG != 5) __syncthreads();  // barrier 2: the twist of block b + 1 is in place
-    f32x2_t rr[kTail > 0 ? kTail : 1], cs[kTail > 0 ? kTail : 1];
-    if (act && FKS_BS_DIAG != 2) {
 #pragma unroll
-      for (int k = kHead; k < kBsSeeds; k++)
-        if (FULL || k < nseeds) lookup(k, rr[k - kHead], cs[k - kHead]);
-    }
-    asm volatile("" ::: "memory");  // the tail's lookups are issued before the row reads
-    uint32_t x1[32], x2[32];
-    bs_load_row(ra_first, x1);  // (the last block re-reads rows it does not use)
-    bs_load_row(ra_second, x2);
-    asm volatile("" ::: "memory");
-    if (act && FKS_BS_DIAG != 2) {
-#pragma unroll
-      for (int k = kHead; k < kBsSeeds; k++)
-        if (FULL || k < nseeds) p = chain(k, p, rr[k - kHead], cs[k - kHead]);
+      for (int k = 0; k < kBsSeeds; k++) {
+        if (FULL || k < nseeds) {
+          f32x2_t rr, cs;
+          lookup(k, rr, cs);
+          p = chain(k, p, rr, cs);
+        }
+        // the lookups of one byte column (8 seeds) at a time: hoisting all 64 table
+        // reads ahead of the chain would spill (pinned lookaheads of 1-8 seeds measured
+        // -0.3..+6.7 %, profiles/r02f_ab_la.log)
+        if ((k % kBsFence) == kBsFence - 1) asm volatile("" ::: "memory");
+      }
       const uint32_t b1v = ST::bits(p.x), b2v = ST::bits(p.y);
       const uint32_t back = swap_adjacent(odd ? b1v : b2v);
       const Pair out = odd ? ST::pack(back, b2v) : ST::pack(b1v, back);
       ST::store_pair(sl.addr, out);
       sl = nxt;
     }
-    temper_rows(x1, x2);
+    __syncthreads();  // barrier 2: the twist of block b + 1 is in place
+    read_rows();
   }
 }
 
@@ -2267,8 +1821,7 @@ __global__ __launch_bounds__(kApplyThreads) void fks_irregular_kernel(IrrArgs a)
   {
     float2* tabCS = reinterpret_cast<float2*>(lds + kLdsCsOff);
     for (int i = tid; i < 256; i += kApplyThreads) {
-      if (FKS_RPAIR) reinterpret_cast<float2*>(lds)[i] = make_float2(c_tab_bf16[i], c_tab_bf16[i]);
-      else reinterpret_cast<float*>(lds)[i] = c_tab_bf16[i];
+      reinterpret_cast<float*>(lds)[i] = c_tab_bf16[i];
       tabCS[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
     }
   }
@@ -2339,6 +1892,99 @@ __global__ __launch_bounds__(kApplyThreads) void fks_irregular_kernel(IrrArgs a)
       __syncthreads();
       ti += n;
       if (n < kApplyThreads) break;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ torch_rocm stream
+// fks_philox_kernel<MODE>: the z stream torch.normal draws on a HIP device (FKS_STREAM_ROCM;
+// PhxTensor in fks_internal.h has the mapping), then the same per-op-rounded update as the
+// CPU stream.  One thread per work item (tensor, idx, j): for every seed in order one
+// Philox4x32-10 call at counter (off4 + j, idx, 0) and key (seed), two rocrand Box-Muller
+// pairs, four elements idx + stride (4 j + i).  Counter-mode: no generator state, no jump.
+__device__ __forceinline__ uint4 philox4x32_10(uint64_t ctr, uint32_t idx, uint64_t seed) {
+  // Random123 Philox4x32-10 as rocrand_philox4x32_10.h:270-303 (counter (x, y, z, w) =
+  // (ctr lo, ctr hi, subsequence lo, hi), key (seed lo, hi), bumped by the Weyl constants)
+  uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32), c2 = idx, c3 = 0u;
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    const uint64_t m0 = (uint64_t)0xD2511F53u * c0, m1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(m1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(m0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)m1;
+    c3 = (uint32_t)m0;
+    c0 = n0;
+    c2 = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return make_uint4(c0, c1, c2, c3);
+}
+
+// rocrand_normal.h:53-68 box_muller as torch's ROCm build compiles it (hipcc's default
+// fp-contract: the uniforms' multiply-add is one fma): (sin * s, cos * s) -- then torch's
+// transformation::normal, val * std + mean with std 1, mean 0 (one fma: -0 becomes +0).
+__device__ __forceinline__ float2 rocrand_box_muller(uint32_t x, uint32_t y) {
+  const float u = __fmaf_rn((float)x, 2.3283064e-10f, 2.3283064e-10f);
+  const float v = __fmaf_rn((float)y, 1.46291807e-09f, 1.46291807e-09f);
+  const float s = sqrtf(-2.0f * logf(u));
+  float sn, cs;
+  __sincosf(v, &sn, &cs);
+  return make_float2(__fmaf_rn(sn * s, 1.0f, 0.0f), __fmaf_rn(cs * s, 1.0f, 0.0f));
+}
+
+template <int DT>
+__device__ __forceinline__ float phx_cast(float v) {  // static_cast<scalar_t>(float)
+  return DT == FKS_F32 ? v : Traits<DT>::rnd(v);
+}
+
+template <int DT, int MODE>
+__device__ __forceinline__ void phx_item(const PhiloxArgs& a, const PhxTensor& T, int64_t r) {
+  using TR = Traits<DT>;
+  const uint32_t S = T.stride;
+  const uint32_t idx = (uint32_t)(r % S);
+  const uint64_t j = (uint64_t)(r / S);
+  int64_t e[4];
+  bool on[4];
+  float p[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    e[i] = (int64_t)idx + (int64_t)S * (int64_t)(4 * j + i);
+    on[i] = e[i] < T.numel;
+    p[i] = (MODE != kModeWriteZ && on[i]) ? TR::load(T.ptr, e[i]) : 0.0f;
+  }
+  const bool has_wd = (T.flags & FKS_HAS_WD) != 0;
+  const bool dv = MODE == kModePerturbUpdate && a.gdev;
+  const bool upd = dv ? dev_value_apply(a.gdev) : true;
+  const float gd = dv ? dev_value_g<DT>(a.gdev) : 0.0f;
+  for (int k = 0; k < a.nseeds; k++) {
+    const uint64_t seed = a.seeds[k];  // wave-uniform: scalar loads
+    const float g = dv ? gd : a.g[3 * k + DT];
+    const uint4 w = philox4x32_10(T.off4 + j, idx, seed);
+    const float2 r1 = rocrand_box_muller(w.x, w.y), r2 = rocrand_box_muller(w.z, w.w);
+    const float rv[4] = {r1.x, r1.y, r2.x, r2.y};
+#pragma unroll
+    for (int i = 0; i < 4; i++) p[i] = apply_one<DT>(p[i], phx_cast<DT>(rv[i]), g, T.lr, T.wd, has_wd, MODE, T.ps, upd);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    if (on[i]) TR::store(T.ptr, e[i], p[i]);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void fks_philox_kernel(PhiloxArgs a) {
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t it = a.item_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; it < a.item_hi; it += step) {
+    int lo = 0, hi = a.nt - 1;  // the last tensor whose first item is <= it
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (a.t[mid].item0 <= it) lo = mid; else hi = mid - 1;
+    }
+    const PhxTensor T = a.t[lo];
+    switch (T.dtype) {
+      case FKS_F32: phx_item<FKS_F32, MODE>(a, T, it - T.item0); break;
+      case FKS_BF16: phx_item<FKS_BF16, MODE>(a, T, it - T.item0); break;
+      default: phx_item<FKS_F16, MODE>(a, T, it - T.item0); break;
     }
   }
 }
@@ -2476,7 +2122,7 @@ static int launch_small2(const ApplyArgs& a, void* stream) {
 template <int DT, int MODE>
 static int launch_apply_t(const ApplyArgs& a, void* stream) {
   if (a.nseeds == kMaxSeedsPerPass) return launch_apply_f<DT, MODE, true>(a, stream);
-  if constexpr (DT == FKS_BF16 && FKS_SM2_TAB == 0 && !FKS_RPAIR) {
+  if constexpr (DT == FKS_BF16) {
     // one-seed bf16 passes with a z-index buffer (fks_capi.cpp ZCache): store / replay
     if (a.zmode == 1 && a.nseeds == 1 && MODE == kModePerturb) return launch_small2<DT, MODE, 1>(a, stream);
     if (a.zmode == 2 && a.nseeds == 1 &&
@@ -2488,8 +2134,8 @@ static int launch_apply_t(const ApplyArgs& a, void* stream) {
     }
   }
   if (a.zmode == 2) return -FKS_ENOTSUP;  // replay without a replay kernel: a host bug
-  if (FKS_SMALL_V2 && a.nseeds <= kSmallK && DT != FKS_F16) return launch_small2<DT == FKS_F16 ? FKS_F32 : DT, MODE>(a, stream);
-  if (FKS_SMALL_DBUF && a.nseeds <= kSmallK) return launch_apply_f<DT, MODE, false, true>(a, stream);
+  if (a.nseeds <= kSmallK && DT != FKS_F16) return launch_small2<DT == FKS_F16 ? FKS_F32 : DT, MODE>(a, stream);
+  if (a.nseeds <= kSmallK) return launch_apply_f<DT, MODE, false, true>(a, stream);  // f16
   return launch_apply_f<DT, MODE, false>(a, stream);
 }
 
@@ -2589,6 +2235,33 @@ __global__ __launch_bounds__(256) void fks_sqrt_domain_kernel(uint32_t* counts) 
 int launch_sqrt_domain_check(uint32_t* counts, void* stream) {
   hipLaunchKernelGGL(fks_sqrt_domain_kernel, dim3(kSqrtDomainBlocks), dim3(256), 0, (hipStream_t)stream, counts);
   return (int)hipGetLastError();
+}
+
+int device_max_threads_per_cu() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 2048;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMaxThreadsPerMultiProcessor, dev) != hipSuccess || n <= 0) return 2048;
+  return n;
+}
+
+template <int MODE>
+static int launch_philox_m(const PhiloxArgs& a, void* stream) {
+  const int64_t items = a.item_hi - a.item_lo;
+  const int64_t blocks = std::min<int64_t>((items + 255) / 256, (int64_t)device_cu_count() * 16);
+  if (blocks <= 0) return 0;
+  hipLaunchKernelGGL((fks_philox_kernel<MODE>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+int launch_philox(const PhiloxArgs& a, void* stream) {
+  if (a.nseeds < 1 || a.nt < 1) return -FKS_EINVAL;
+  switch (a.mode) {
+    case kModeUpdate: return launch_philox_m<kModeUpdate>(a, stream);
+    case kModePerturb: return launch_philox_m<kModePerturb>(a, stream);
+    case kModePerturbUpdate: return launch_philox_m<kModePerturbUpdate>(a, stream);
+    case kModeWriteZ: return launch_philox_m<kModeWriteZ>(a, stream);
+    default: return -FKS_ENOTSUP;
+  }
 }
 
 int launch_irregular(const IrrArgs& a, void* stream) {

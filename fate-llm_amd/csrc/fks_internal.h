@@ -84,32 +84,20 @@ struct DevTiny {
 static_assert(sizeof(DevTiny) == 40, "DevTiny layout");
 
 constexpr int kApplyThreads = 320;  // 312 Box-Muller pairs per 624-word block + 8 idle lanes
-#ifndef FKS_APPLY_WG_PER_CU
-#define FKS_APPLY_WG_PER_CU 3
-#endif
-constexpr int kApplyWgPerCu = FKS_APPLY_WG_PER_CU;  // resident apply workgroups per CU (LDS-limited)
+constexpr int kApplyWgPerCu = 3;  // resident apply workgroups per CU (LDS-limited)
 // MT windows resident in LDS per workgroup: (seeds + 1 spare) x 2496 B + 4 KB tables <= 160 KB / WGs
 constexpr int kMaxSeedsPerPass = (160 * 1024 / kApplyWgPerCu - 4096) / 2496 - 1;  // tables: <= 4 KB
 // calls of at most kSmallK seeds run one pass over kSmallWgPerCu workgroups per CU
 constexpr int kSmallK = 4;
-#ifndef FKS_SMALL_V2
-#define FKS_SMALL_V2 1  // passes of <= kSmallK seeds over fast segments: fks_small2_kernel (two pairs per lane)
-#endif
-#ifndef FKS_SMALL_WG_PER_CU
-#define FKS_SMALL_WG_PER_CU (FKS_SMALL_V2 ? 8 : 5)
-#endif
-// v1 (FKS_SMALL_V2=0): 62-68 VGPRs (7 waves/SIMD), 5 workgroups of 5 waves; measured per
-// K=1 pass over the 7B layout: 4 WGs 14.5 ms, 5 WGs 12.9 ms, 6 WGs 18.6 ms.
-// v2: 56 VGPRs, 8 workgroups of 4 waves (8 waves/SIMD; K = 1, 2 fit 8 in LDS, K = 4 six):
-// perturb 7.2 ms at 8 WGs, 7.8 ms at 6 (profiles/r02_smallk_ab.log)
-constexpr int kSmallWgPerCu = FKS_SMALL_WG_PER_CU;
+// fks_small2_kernel (two Box-Muller pairs per lane): 56 VGPRs, 8 workgroups of 4 waves
+// (8 waves/SIMD; K = 1, 2 fit 8 in LDS, K = 4 six): perturb 7.2 ms at 8 WGs, 7.8 ms at 6
+// (profiles/r02_smallk_ab.log; the round-1 kernel of one pair per lane: 9.1 ms)
+constexpr int kSmallWgPerCu = 8;
 // one-seed bf16 z indices (fks_small2_kernel ZM 1 / 2): one u32 per pair lane and block
 constexpr int kSm2ZidxPerBlock = 156;
 constexpr int kSm2ZidxBytesPerBlock = 4 * kSm2ZidxPerBlock;
 constexpr int kJumpThreads = 1024;  // 16 waves, one chunk's jump per wave at a time
-#ifndef FKS_JUMP_MAX_CPW
-#define FKS_JUMP_MAX_CPW 32  // most chunks one jump workgroup takes (fks_capi.cpp jump_chunks_per_wg)
-#endif
+constexpr int kJumpMaxCpw = 32;  // most chunks one jump workgroup takes (fks_capi.cpp jump_chunks_per_wg)
 constexpr int kJumpXLen = 19937 + 624;  // x[0..20560]: y[i + w] = x[i + w + 1], i < 19937, w < 624
 
 // kModeUpdateWd / kModeUpdateNoWd: kModeUpdate specialised for a launch whose segments
@@ -194,6 +182,45 @@ struct JumpArgs {
   int32_t nchunks;
   int32_t chunks_per_wg;
 };
+
+// ---- torch_rocm stream (FKS_STREAM_ROCM): torch.normal on a HIP device ----
+// torch's normal_kernel (ATen/native/cuda/DistributionTemplates.h:444-471) draws through
+// distribution_nullary_kernel (:97-160): a grid-stride loop of `stride` = 256 x grid
+// threads (calc_execution_policy :50-62: grid = min(ceil(numel / 256), CUs x
+// maxThreadsPerCU / 256)), thread idx drawing curand_normal4 (Philox4x32-10 at
+// subsequence idx, offset `philox offset`; Box-Muller of rocrand) once per loop
+// iteration j for the elements idx + stride (4 j + i), i < 4.  Each tensor's draw
+// advances the generator's offset by ((numel - 1) / (4 stride) + 1) * 4.
+// A work ITEM is one (tensor, idx, j): one Philox call, four elements.
+struct PhxTensor {
+  uint64_t ptr;     // device address of element 0
+  int64_t numel;
+  int64_t item0;    // the tensor's first work item (items of all tensors laid end to end)
+  uint64_t off4;    // philox offset / 4 of this tensor's draw (the counter's 64-bit low half)
+  uint32_t stride;  // 256 x grid of torch's launch
+  int32_t dtype;
+  float lr;
+  float wd;
+  uint32_t flags;   // FKS_HAS_WD | FKS_FROZEN
+  float ps;         // perturbation scale (perturb modes)
+};
+static_assert(sizeof(PhxTensor) == 56, "PhxTensor layout");
+
+constexpr int kPhxSeeds = 32;  // seeds per launch (by value in the arguments)
+struct PhiloxArgs {
+  uint64_t seeds[kPhxSeeds];
+  float g[kPhxSeeds * 3];  // the multiplier per seed, per dtype
+  const PhxTensor* t;   // sorted by item0
+  const float* gdev;    // kModePerturbUpdate from device memory: {g, apply} (nullptr: g[] above)
+  int64_t item_lo;      // this launch's items [item_lo, item_hi) (element shards)
+  int64_t item_hi;
+  int32_t nt;
+  int32_t nseeds;
+  int32_t mode;
+  int32_t pad;
+};
+int launch_philox(const PhiloxArgs& a, void* stream);
+int device_max_threads_per_cu();
 
 // fks_delta_apply: p = dtype(f32(decay) * p - delta[delta_off + e]) over one tensor
 struct DeltaApplyDesc {

@@ -11,9 +11,17 @@ Three operations, each replacing one reference routine (include/fks.h has the AB
 * ``normal_``          -- the torch.normal(mean=0, std=1, size, dtype) draws the two
   routines above make after torch.manual_seed(seed) (zo_utils.py:47, optimizer.py:170).
 
-The z stream is the one the reference produces on CPU tensors (torch's mt19937 +
-normal_fill), regenerated on the GPU; updates are applied in place (the reference
-rebinds ``param.data`` to a new tensor of identical values).
+The z stream (``stream_mode``) is the one the reference draws where its parameters live
+(zo_utils.py:47 and optimizer.py:170-172 draw on ``param.data.device``):
+
+* ``"torch_cpu"`` (default): torch's CPU generator, mt19937 + normal_fill -- a reference
+  client that trains on the CPU (the FedKSeed tutorial's configuration);
+* ``"torch_rocm"``: torch's HIP-device generator, Philox4x32-10 + rocrand's Box-Muller in
+  torch's grid-stride mapping -- a reference client whose model sits on an MI355X.
+
+All parties of one federation must draw the same stream; the
+default comes from ``FKS_STREAM_MODE`` and ``set_stream_mode``.  Updates are applied in
+place (the reference rebinds ``param.data`` to a new tensor of identical values).
 
 There is no CPU path: tensors must live on a HIP device and libfks.so must be
 loadable, otherwise these functions raise.
@@ -33,6 +41,29 @@ import torch
 from . import _native as N
 
 _DTYPES = {torch.float32: N.F32, torch.bfloat16: N.BF16, torch.float16: N.F16}
+STREAM_MODES = ("torch_cpu", "torch_rocm")
+_stream_mode = os.environ.get("FKS_STREAM_MODE", "torch_cpu")
+if _stream_mode not in STREAM_MODES:
+    raise ValueError(f"FKS_STREAM_MODE must be one of {STREAM_MODES}, not {_stream_mode!r}")
+
+
+def set_stream_mode(mode: str) -> None:
+    """The z stream every codec call draws unless told otherwise (module docstring)."""
+    global _stream_mode
+    if mode not in STREAM_MODES:
+        raise ValueError(f"stream_mode must be one of {STREAM_MODES}, not {mode!r}")
+    _stream_mode = mode
+
+
+def get_stream_mode() -> str:
+    return _stream_mode
+
+
+def _mode(stream_mode) -> str:
+    m = _stream_mode if stream_mode is None else stream_mode
+    if m not in STREAM_MODES:
+        raise ValueError(f"stream_mode must be one of {STREAM_MODES}, not {m!r}")
+    return m
 
 
 @dataclass
@@ -52,8 +83,10 @@ def _f32(x: float) -> float:
 class _Batch:
     """fks_tensor array for a list of specs (keeps contiguous staging copies alive)."""
 
-    def __init__(self, specs: Sequence[ParamSpec]):
+    def __init__(self, specs: Sequence[ParamSpec], stream_mode=None):
         self.specs = list(specs)
+        self.stream_mode = _mode(stream_mode)
+        stream_flag = N.STREAM_ROCM if self.stream_mode == "torch_rocm" else 0
         self.copies = []  # (original, contiguous staging) pairs to write back
         self.device = None
         arr = (N.FksTensor * max(1, len(self.specs)))()
@@ -75,7 +108,7 @@ class _Batch:
             arr[i].data = t.data_ptr() if t.numel() else None
             arr[i].numel = t.numel()
             arr[i].dtype = _DTYPES[t.dtype]
-            flags = 0
+            flags = stream_flag
             if sp.weight_decay is not None:
                 flags |= N.HAS_WD
             if sp.frozen:
@@ -113,16 +146,17 @@ def _seed_u64(s) -> int:
 
 
 def directional_step(specs: Sequence[ParamSpec], seeds: Sequence[int], values: Sequence[float],
-                     value_is_tensor: bool = False, shard: int = 0, nshards: int = 1) -> None:
+                     value_is_tensor: bool = False, shard: int = 0, nshards: int = 1, stream_mode=None) -> None:
     """For each (seed, value) in order: p <- p - lr*(value*z + wd*p) over ``specs``.
 
-    ``shard``/``nshards``: only the shard-th of nshards equal runs of MT19937 blocks of
-    the parameter stream is updated (element sharding across ranks; bit-identical)."""
+    ``shard``/``nshards``: only the shard-th of nshards equal parts of the parameter stream
+    is updated (element sharding across ranks; bit-identical): runs of MT19937 blocks
+    (torch_cpu) or of Philox work items (torch_rocm)."""
     if len(seeds) != len(values):
         raise ValueError("seeds and values differ in length")
     if not specs or not len(seeds):
         return
-    b = _Batch(specs)
+    b = _Batch(specs, stream_mode)
     if b.device is None:
         return
     L = N.load()
@@ -183,7 +217,7 @@ def zindex_release(device=None) -> None:
             del _zindex[idx]
 
 
-def perturb(tensors: Sequence[torch.Tensor], seed: int, scales) -> None:
+def perturb(tensors: Sequence[torch.Tensor], seed: int, scales, stream_mode=None) -> None:
     """p <- p + scale_i*z for every tensor i (scale = scaling_factor*eps of its group, a
     python double); ``scales`` is one number for all tensors or one per tensor."""
     specs = [ParamSpec(t) for t in tensors]
@@ -193,13 +227,14 @@ def perturb(tensors: Sequence[torch.Tensor], seed: int, scales) -> None:
         scales = [float(scales)] * len(specs)
     if len(scales) != len(specs):
         raise ValueError("one scale per tensor")
-    b = _Batch(specs)
+    b = _Batch(specs, stream_mode)
     if b.device is None:
         return
     L = N.load()
     sc = np.ascontiguousarray([float(x) for x in scales], dtype=np.float64)
     with torch.cuda.device(b.device):
-        zindex_reserve(b)
+        if b.stream_mode == "torch_cpu":
+            zindex_reserve(b)
         ws, nbytes = b.workspace(1)
         N.check(L.fks_perturb(ctypes.addressof(b.arr), b.n, _seed_u64(seed), sc.ctypes.data, ws.data_ptr(), nbytes,
                               _stream_handle(b.device)))
@@ -207,7 +242,7 @@ def perturb(tensors: Sequence[torch.Tensor], seed: int, scales) -> None:
 
 
 def perturb_step(specs: Sequence[ParamSpec], seed: int, scales: Sequence[float], value: float,
-                 value_is_tensor: bool = True, update: bool = True) -> None:
+                 value_is_tensor: bool = True, update: bool = True, stream_mode=None) -> None:
     """zeroth_order_step's restore perturbation fused with its directional step, in one
     device pass: p <- p + scale_i*z, then (``update``) p <- p - lr*(value*z + wd*p) with
     the same z.  Equal, bit for bit, to ``perturb`` followed by ``directional_step``
@@ -217,7 +252,7 @@ def perturb_step(specs: Sequence[ParamSpec], seed: int, scales: Sequence[float],
         return
     if len(scales) != len(specs):
         raise ValueError("one scale per tensor")
-    b = _Batch(specs)
+    b = _Batch(specs, stream_mode)
     if b.device is None:
         return
     L = N.load()
@@ -231,7 +266,7 @@ def perturb_step(specs: Sequence[ParamSpec], seed: int, scales: Sequence[float],
 
 
 def perturb_step_device(specs: Sequence[ParamSpec], seed: int, scales: Sequence[float], value: torch.Tensor,
-                        apply: torch.Tensor) -> None:
+                        apply: torch.Tensor, stream_mode=None) -> None:
     """``perturb_step`` with ``value`` (g) and ``apply`` (bool) as device tensors read by the
     kernels when they run: the restore perturbation always, the update iff ``apply`` --
     no host synchronisation on the losses.  g is rounded to each tensor's dtype like a
@@ -241,7 +276,7 @@ def perturb_step_device(specs: Sequence[ParamSpec], seed: int, scales: Sequence[
         return
     if len(scales) != len(specs):
         raise ValueError("one scale per tensor")
-    b = _Batch(specs)
+    b = _Batch(specs, stream_mode)
     if b.device is None:
         return
     if value.device != b.device or apply.device != b.device:
@@ -256,12 +291,13 @@ def perturb_step_device(specs: Sequence[ParamSpec], seed: int, scales: Sequence[
         b.finish()
 
 
-def normal_(tensors: Sequence[torch.Tensor], seed: int, frozen: Optional[Sequence[bool]] = None) -> None:
+def normal_(tensors: Sequence[torch.Tensor], seed: int, frozen: Optional[Sequence[bool]] = None,
+            stream_mode=None) -> None:
     """Overwrite every tensor with the z the reference draws for it after manual_seed(seed)."""
     specs = [ParamSpec(t, frozen=bool(frozen[i]) if frozen else False) for i, t in enumerate(tensors)]
     if not specs:
         return
-    b = _Batch(specs)
+    b = _Batch(specs, stream_mode)
     if b.device is None:
         return
     L = N.load()

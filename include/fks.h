@@ -57,6 +57,12 @@ extern "C" {
 #define FKS_HAS_WD 1u   /* weight decay term present: p - lr*(g*z + wd*p)  (zo_utils.py:49)
                            absent:                    p - lr*(g*z)         (zo_utils.py:52)   */
 #define FKS_FROZEN 2u   /* draws its z (stream advances) but the tensor is not written         */
+#define FKS_STREAM_ROCM 4u  /* z stream: torch's HIP-device generator (Philox4x32-10 + rocrand
+                           Box-Muller, torch/include/ATen/native/cuda/DistributionTemplates.h:
+                           50-160, 444-471) -- the stream a reference client whose model sits on
+                           a GPU draws (zo_utils.py:47 and optimizer.py:170-172 draw on
+                           param.data.device).  Without it: torch's CPU generator (mt19937 +
+                           normal_fill).  Every tensor of one call must agree. */
 
 /* error codes (negated) */
 #define FKS_EINVAL 22

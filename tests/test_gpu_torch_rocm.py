@@ -1,0 +1,118 @@
+"""The torch_rocm z stream (FKS_STREAM_ROCM): a reference client whose model sits on a GPU
+draws z on the device (zo_utils.py:47 and optimizer.py:170-172 pass
+``device=param.data.device``), i.e. torch's HIP generator -- Philox4x32-10 with rocrand's
+Box-Muller in torch's grid-stride mapping (ATen/native/cuda/DistributionTemplates.h).
+The oracle for this stream is torch itself on the same GPU (the installed PyTorch-ROCm,
+not the reference): after torch.manual_seed(seed), torch.normal(..., device="cuda") for
+each tensor in order, and the reference's update expression as torch ops on the device
+(oracle/torch_replica.py).  Bar: bit-exact.
+
+Cases: fp32 / bf16 / f16; tensors below one 256-thread block, between blocks, past the
+grid cap (several Philox calls per thread), empty tensors in the list (no draw, no
+offset); several seeds including 0, 2^32-1 and one past 2^32; reconstructs at weight
+decay 0.01 / 0.0 / None with zero scalars skipped; the perturb +1/-2/+1 sequence with a
+frozen tensor; element shards."""
+import pytest
+import torch
+
+from oracle import torch_replica as R
+from test_gpu_parity import _dev
+
+pytestmark = pytest.mark.gpu
+
+DT = {"float32": torch.float32, "bfloat16": torch.bfloat16, "float16": torch.float16}
+SHAPES = [(1,), (7,), (256,), (1000,), (4097,), (0,), (33, 65), (600_000,), (3_000_001,), (16,)]
+
+
+def _bits(t):
+    return t.view(torch.int16) if t.element_size() == 2 else t.view(torch.int32)
+
+
+def _assert_same(got, want, what):
+    if not torch.equal(_bits(got), _bits(want)):
+        bad = (_bits(got) != _bits(want)).nonzero()
+        i = bad[0].tolist()
+        raise AssertionError(f"{what}: {bad.shape[0]} of {got.numel()} elements differ, first at {i}: "
+                             f"{got[tuple(i)].item()} vs {want[tuple(i)].item()}")
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16", "float16"])
+@pytest.mark.parametrize("seed", [0, 42, 2**32 - 1, 2**40 + 3])
+def test_normal_stream_matches_torch_on_device(dtype, seed):
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    torch.manual_seed(seed)
+    want = [torch.normal(mean=0, std=1, size=s, device=dev, dtype=DT[dtype]) for s in SHAPES]
+    got = [torch.empty(s, device=dev, dtype=DT[dtype]) for s in SHAPES]
+    codec.normal_(got, seed, stream_mode="torch_rocm")
+    torch.cuda.synchronize()
+    for s, g, w in zip(SHAPES, got, want):
+        _assert_same(g, w, f"seed {seed} shape {s}")
+
+
+def _params(dtype, dev, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    shapes = [(4096,), (48,), (1000, 17), (700_001,), (0,), (9,)]
+    return [(torch.randn(s, generator=g) * 0.02).to(DT[dtype]).to(dev) for s in shapes]
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("wd", [0.01, 0.0, None])
+def test_reconstruct_matches_torch_on_device(dtype, wd):
+    """ClientTrainer.train_once's loop (fedkseed.py:136-141) run by the reference's own
+    arithmetic on the GPU vs the codec's reconstruct in the torch_rocm stream."""
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    g = torch.Generator().manual_seed(7)
+    seeds = torch.randint(0, 2**32, (40,), generator=g).tolist()
+    vals = (torch.randn(40, generator=g, dtype=torch.float64) * 20).tolist()
+    vals[5] = 0.0
+    ref = _params(dtype, dev)
+    got = [p.clone() for p in ref]
+    R.reconstruct(ref, seeds, vals, 1e-3, wd)
+    keep = [(s, v) for s, v in zip(seeds, vals) if v != 0.0]
+    specs = [codec.ParamSpec(p, lr=1e-3, weight_decay=wd) for p in got]
+    codec.directional_step(specs, [s for s, _ in keep], [v for _, v in keep], stream_mode="torch_rocm")
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(zip(got, ref)):
+        _assert_same(a, b, f"tensor {i}")
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_perturb_sequence_with_frozen_tensor(dtype):
+    """random_perturb_parameters (optimizer.py:152-173) +1, -2, +1: frozen tensors draw
+    nothing; the restore is not bit-exact (three roundings), the same in both."""
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    ref = _params(dtype, dev, seed=3)
+    frozen = [False, True, False, False, False, False]
+    got = [p.clone() for p in ref]
+    eps, seed = 5e-4, 123456789
+    for sf in (1.0, -2.0, 1.0):
+        torch.manual_seed(seed)
+        for p, fz in zip(ref, frozen):
+            if not fz:
+                z = torch.normal(mean=0, std=1, size=p.size(), device=p.device, dtype=p.dtype)
+                p.data = p.data + sf * eps * z
+        codec.perturb([p for p, fz in zip(got, frozen) if not fz], seed, sf * eps, stream_mode="torch_rocm")
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(zip(got, ref)):
+        _assert_same(a, b, f"tensor {i}")
+
+
+def test_element_shards_equal_whole():
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    g = torch.Generator().manual_seed(9)
+    seeds = torch.randint(0, 2**32, (35,), generator=g).tolist()
+    vals = (torch.randn(35, generator=g, dtype=torch.float64) * 20).tolist()
+    whole = _params("bfloat16", dev, seed=5)
+    shards = [p.clone() for p in whole]
+    codec.directional_step([codec.ParamSpec(p, lr=1e-3, weight_decay=0.01) for p in whole], seeds, vals,
+                           stream_mode="torch_rocm")
+    sp = [codec.ParamSpec(p, lr=1e-3, weight_decay=0.01) for p in shards]
+    for r in range(3):
+        codec.directional_step(sp, seeds, vals, shard=r, nshards=3, stream_mode="torch_rocm")
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(zip(shards, whole)):
+        _assert_same(a, b, f"tensor {i}")
