@@ -5,18 +5,24 @@ One "step" = one reconstruct of the LLaMA-7B-shaped bf16 parameter buffer
 (seed, scalar) pairs -- the loop of ClientTrainer.train_once (fedkseed.py:136-141)
 -- device-resident, through the drop-in fate_llm.algo.fedkseed codec (libfks.so).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode sequential|seed-shard] [--gather]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode sequential|seed-shard]
+                  [--scaling weak|strong] [--gather]
 
 --gpus N > 1 without WORLD_SIZE in the environment re-launches this script under
 torch.distributed.run with N ranks (one per GPU, 127.0.0.1) as a CHILD process, before
 anything touches the GPU, and exits with its status; run under torch.distributed.run
 directly, WORLD_SIZE must equal --gpus.
 
---mode sequential (default, bit-exact): the parameter stream is cut into N equal runs of
-MT19937 blocks and rank r reconstructs run r (element sharding: every element still sees
-every seed in order, so the union is bit-identical to N = 1 and no collective touches the
-data path).  --gather adds the all-gather that leaves the whole buffer on every rank (N
-RCCL broadcasts of the shards), timed separately.  Total work is fixed: "strong" scaling.
+--mode sequential (default, bit-exact):
+  --scaling weak (default): every rank reconstructs its own 7B buffer from the same
+    K=4096 list -- the FedKSeed deployment, where each client GPU rebuilds its model from
+    the (seed, sum) list the arbiter broadcasts (fedkseed.py:128-141); no collective;
+    value = N buffers / the slowest rank's time;
+  --scaling strong: one 7B buffer cut into N equal runs of MT19937 blocks, rank r
+    reconstructs run r (element sharding: every element still sees every seed in order,
+    so the union is bit-identical to N = 1 and no collective touches the data path);
+    --gather adds the all-gather that leaves the whole buffer on every rank (N RCCL
+    broadcasts of the shards), timed separately.
 
 --mode seed-shard: the north star's C3 variant.  Rank r takes a contiguous 1/N of the
 seeds, accumulates its f32 delta over the whole buffer (fks_delta_accumulate), one RCCL
@@ -316,20 +322,22 @@ def run(args, world, rank, local):
     if seed_shard:
         groups = [{"params": views, "lr": 1e-5, "weight_decay": wd}]
         delta = torch.empty(total, dtype=torch.float32, device=dev)
-    shard_words = [codec.shard_range(specs, r, world) for r in range(world)] if world > 1 else [(0, total)]
+    weak = not seed_shard and args.scaling == "weak"
+    nshards = 1 if weak else world
+    shard_words = [codec.shard_range(specs, r, nshards) for r in range(nshards)] if nshards > 1 else [(0, total)]
 
     def step():
         if seed_shard:
             zo_utils.reconstruct_seed_sharded_(groups, ks, kv, lr=1e-5, weight_decay=wd, delta=delta)
         else:
-            codec.directional_step(specs, ks, kv, shard=rank, nshards=world)
+            codec.directional_step(specs, ks, kv, shard=rank % nshards, nshards=nshards)
 
     sync = torch.cuda.synchronize
     with codec.profile() as prof:
         dt = timed_steps(step, args, world, sync)
     dt = max_over_ranks(dt, world, dev)
     gather_ms = None
-    if args.gather and world > 1 and not seed_shard:
+    if args.gather and world > 1 and not seed_shard and not weak:
         # every rank ends with the whole buffer: one broadcast of each element shard (the
         # bench's buffer is one flat tensor and all its tensors are fast segments, so a
         # shard's stream words are its element range)
@@ -355,13 +363,13 @@ def run(args, world, rank, local):
                "value": round(total * 2 / alt_s / 1e9, 4), "steps": 1}
 
     ms_per_step = dt / args.steps * 1e3
-    buf_bytes = total * 2
+    buf_bytes = total * 2 * (world if weak else 1)  # weak: one buffer per rank
     value = buf_bytes / (dt / args.steps) / 1e9
 
     # ---- rooflines of the dominant kernel, this rank: the bf16 slice kernel
     # (fks_apply_bs_kernel, 32 seeds per launch) for every reconstruct of >= 20 seeds
     n_steps_prof = args.steps + args.warmup
-    rank_params = total if seed_shard else (shard_words[rank][1] - shard_words[rank][0])
+    rank_params = total if seed_shard else (shard_words[rank % nshards][1] - shard_words[rank % nshards][0])
     n_apply = max(prof.n_apply, 1)
     avg_apply_s = prof.apply_ms / n_apply / 1e3
     rank_seeds = len(ks) * (rank + 1) // world - len(ks) * rank // world if seed_shard else len(ks)
@@ -405,8 +413,8 @@ def run(args, world, rank, local):
     # buffer once, SURVEY.md §8(d): 2 N elt) over the reconstruct time; the per-pass figure
     # (each 32-seed launch streams its shard once) is reported beside it, named as such
     elt = 4 if seed_shard else 2
-    alg_bytes_step = 2 * total * 2
-    hbm_ach = alg_bytes_step / (dt / args.steps) / 1e9
+    alg_bytes_step = 2 * total * 2 * (world if weak else 1)
+    hbm_ach = alg_bytes_step / (dt / args.steps) / 1e9 / world  # per GPU, against one GPU's peak
     traffic = pmc.get("hbm_bytes_per_param_per_launch")
     hbm = {"bound": "hbm", "achieved": round(hbm_ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(hbm_ach / HBM_PEAK_GBS, 7),
@@ -419,16 +427,19 @@ def run(args, world, rank, local):
     out = {
         "metric": "GB/s param buffer reconstructed from (seed,scalar) list, device-resident",
         "value": round(value, 4), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 2), "higher_is_better": True, "scaling": "strong",
+        "ms_per_step": round(ms_per_step, 2), "higher_is_better": True, "scaling": "weak" if weak else "strong",
         "mode": args.mode, "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic (random-init LLaMA-7B shapes, seeded seeds/scalars)",
         "config": {"workload": (f"{world}xMI355X: same 7B / K={args.k}, seeds sharded {len(ks) // world}/GPU, "
                                 f"RCCL all-reduce of delta over xGMI") if seed_shard else
                    "1xMI355X: 7B-param bf16 buffer, K=4096 seeds" if world == 1 else
+                   (f"{world}xMI355X: one 7B-param bf16 buffer per GPU, K=4096 seeds (each GPU one client's "
+                    "reconstruct, no collective)") if weak else
                    f"{world}xMI355X: 7B-param bf16 buffer, K=4096 seeds, element-sharded (bit-exact, no collective)",
                    "params": total, "k": args.k, "k_nonzero": len(ks), "tensors": len(shapes),
                    "lr": 1e-5, "weight_decay": wd,
-                   "parallelism": f"seed-shard{world}" if seed_shard else f"element-shard{world}"},
+                   "parallelism": (f"seed-shard{world}" if seed_shard else
+                                   f"client-per-gpu{world}" if weak else f"element-shard{world}")},
         "roofline": valu if valu else hbm,
         "roofline_hbm": hbm,
         "build_id": build_id,
@@ -468,7 +479,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=24.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("sequential", "seed-shard"), default="sequential")
-    ap.add_argument("--gather", action="store_true", help="N > 1, sequential: all-gather the shards afterwards")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="sequential mode, N > 1: weak = a 7B buffer per GPU (default), strong = one buffer "
+                         "element-sharded over the GPUs")
+    ap.add_argument("--gather", action="store_true", help="N > 1, strong: all-gather the shards afterwards")
     ap.add_argument("--selftest", action="store_true", help="CPU/gloo check of the launcher and timing logic")
     args = ap.parse_args()
 
