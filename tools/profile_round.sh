@@ -1,16 +1,17 @@
 #!/bin/bash
 # One GPU call for a round's measurement set (repo root on the GPU box):
-#   TAG=r02 bash tools/profile_round.sh
-# 1) PMC passes of the slice kernel (tools/gpu_pmc2.sh) -> profiles/pmc_apply_${TAG}_${PMCV}.json
-#    (PMCV wd0, the default: the bench's weight decay 0.0; full: wd 0.01)
+#   TAG=r03 bash tools/profile_round.sh
+# 1) PMC passes of the slice kernel (tools/gpu_pmc2.sh) -> profiles/pmc_apply_${TAG}_{wd0,full}.json
+#    (wd0: the bench's weight decay 0.0; full: wd 0.01), each carrying the build id of the
+#    libfks.so it profiled (bench.py uses a summary only for the same build)
 # 2) the default bench line (N=1, with cpu_baseline)      -> gpurun_out/${TAG}_bench_default.log
 # 3) rocprofv3 --kernel-trace --stats of one bench step   -> gpurun_out/${TAG}_trace/
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-TAG=${TAG:-r02}
-PMCV=${PMCV:-wd0}
-TAG=$TAG VARIANTS=$PMCV timeout -k 10 400 bash tools/gpu_pmc2.sh > gpurun_out/${TAG}_pmc.log 2>&1 || { tail gpurun_out/${TAG}_pmc.log; exit 91; }
-cp profiles/pmc_apply_${TAG}_${PMCV}.json gpurun_out/ 2>/dev/null
-timeout -k 10 300 python3 -u bench.py > gpurun_out/${TAG}_bench_default.log 2>&1 || { tail gpurun_out/${TAG}_bench_default.log; exit 92; }
+TAG=${TAG:-r03}
+PMCV=${PMCV:-wd0 full}
+TAG=$TAG VARIANTS="$PMCV" timeout -k 10 600 bash tools/gpu_pmc2.sh > gpurun_out/${TAG}_pmc.log 2>&1 || { tail gpurun_out/${TAG}_pmc.log; exit 91; }
+for v in $PMCV; do cp profiles/pmc_apply_${TAG}_$v.json gpurun_out/ 2>/dev/null; done
+timeout -k 10 400 python3 -u bench.py > gpurun_out/${TAG}_bench_default.log 2>&1 || { tail gpurun_out/${TAG}_bench_default.log; exit 92; }
 tail -1 gpurun_out/${TAG}_bench_default.log
 rm -rf gpurun_out/${TAG}_trace
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace -o run --output-format csv -- \
