@@ -24,6 +24,8 @@
 
 #include "fks_internal.h"
 #include "fks_bitslice.h"
+#define FKS_HD __device__ __forceinline__
+#include "fks_libm.h"
 
 // Design choices measured on MI355X in rounds 1-2 are fixed in the code; the A/B knobs
 // and the wrong-result timing diagnostics of those rounds were removed (their logs are
@@ -1797,9 +1799,11 @@ __device__ __forceinline__ void irr_tiny_lane(const uint32_t* win, const IrrArgs
   for (int k = 0; k < a.nseeds; k++) {
     const double u1 = u53(mt_temper(win_word(win, k, w)), mt_temper(win_word(win, k, w + 1)));
     const double u2 = u53(mt_temper(win_word(win, k, w + 2)), mt_temper(win_word(win, k, w + 3)));
-    const double r = sqrt(-2.0 * log1p(-u2));
+    // glibc's log1p and correctly rounded sin / cos (fks_libm.h): ocml's differ from the
+    // host libm by an ulp often enough to flip fp32 midpoint cases
+    const double r = sqrt(-2.0 * fks_libm::log1p(-u2));
     const double theta = 2.0 * 3.14159265358979323846 * u1;
-    const double v = (sin_half ? r * sin(theta) : r * cos(theta)) * 1.0 + 0.0;
+    const double v = r * fks_libm::sin_or_cos(theta, sin_half) * 1.0 + 0.0;
     const float zf = (float)v;  // static_cast<scalar_t>(double): via float for bf16 / f16
     const float z = DT == FKS_F32 ? zf : Traits<DT>::rnd(zf);
     p = apply_one<DT>(p, z, dv ? dev_value_g<DT>(a.gdev) : g[k], T.lr, T.wd, has_wd, MODE, T.ps, upd);

@@ -1,0 +1,78 @@
+// Host checker for fate-llm_amd/csrc/fks_libm.h (test infrastructure, built by
+// tests/test_libm_serial.py with g++ -O2 -ffp-contract=off): the header's log1p / sin /
+// cos against this host's glibc, which is what the reference's CPU z stream calls.
+//   libm_check log1p N      -> "bad <count>" over N inputs -u2, u2 = m 2^-53
+//   libm_check sincos N     -> "bad <count>" then up to 256 "theta mine glibc" hex lines
+//   libm_check z            -> stdin "a b which" (53-bit hex, which 0 = cos, 1 = sin);
+//                              stdout the fp32 bits of the serial-path z, header and glibc
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../fate-llm_amd/csrc/fks_libm.h"
+
+static uint64_t xs = 88172645463325252ull;
+static uint64_t next() {
+  xs ^= xs << 13;
+  xs ^= xs >> 7;
+  xs ^= xs << 17;
+  return xs;
+}
+static double u53(uint64_t m) { return (double)(m & ((1ull << 53) - 1)) * (1.0 / 9007199254740992.0); }
+
+int main(int argc, char** argv) {
+  if (argc < 2) return 2;
+  if (!strcmp(argv[1], "log1p")) {
+    const long n = atol(argv[2]);
+    long bad = 0;
+    for (long i = 0; i < n; i++) {
+      uint64_t m = next() & ((1ull << 53) - 1);
+      if (i % 4 == 1) m >>= (next() >> 58);  // small u2 as well
+      const double x = -u53(m);
+      if (fks_libm::bits(fks_libm::log1p(x)) != fks_libm::bits(log1p(x))) bad++;
+    }
+    printf("bad %ld\n", bad);
+    return 0;
+  }
+  if (!strcmp(argv[1], "sincos")) {
+    const long n = atol(argv[2]);
+    long bad = 0;
+    for (long i = 0; i < n; i++) {
+      uint64_t m = next() & ((1ull << 53) - 1);
+      if (i % 8 == 1) m >>= (next() >> 58);
+      const double th = 2.0 * 3.14159265358979323846 * u53(m);
+      for (int s = 0; s < 2; s++) {
+        const double mine = fks_libm::sin_or_cos(th, s), ref = s ? sin(th) : cos(th);
+        if (fks_libm::bits(mine) != fks_libm::bits(ref)) {
+          if (bad < 256)
+            fprintf(stderr, "%d %016llx %016llx %016llx\n", s, (unsigned long long)fks_libm::bits(th),
+                    (unsigned long long)fks_libm::bits(mine), (unsigned long long)fks_libm::bits(ref));
+          bad++;
+        }
+      }
+    }
+    printf("bad %ld\n", bad);
+    return 0;
+  }
+  if (!strcmp(argv[1], "z")) {
+    unsigned long long a, b;
+    int which;
+    while (scanf("%llx %llx %d", &a, &b, &which) == 3) {
+      const double u1 = u53(a), u2 = u53(b);
+      const double th = 2.0 * 3.14159265358979323846 * u1;
+      const double r1 = sqrt(-2.0 * fks_libm::log1p(-u2));
+      const double v1 = r1 * fks_libm::sin_or_cos(th, which) * 1.0 + 0.0;
+      const double r2 = sqrt(-2.0 * log1p(-u2));
+      const double v2 = r2 * (which ? sin(th) : cos(th)) * 1.0 + 0.0;
+      const float f1 = (float)v1, f2 = (float)v2;
+      uint32_t b1, b2;
+      memcpy(&b1, &f1, 4);
+      memcpy(&b2, &f2, 4);
+      printf("%08x %08x\n", b1, b2);
+    }
+    return 0;
+  }
+  return 2;
+}
