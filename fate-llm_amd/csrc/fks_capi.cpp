@@ -565,7 +565,14 @@ CachedPlan* build_plan(const fks_tensor* t, int nt, const double* scales, uint64
   if (C->have_reg) P = make_plan(br, small);
   Plan BP;
   C->have_bs = !small && !L.segs[FKS_BF16].empty();
-  if (C->have_bs) BP = make_plan_n(br, bs_nchunks(br.hi - br.lo));
+  if (C->have_bs) {
+    BP = make_plan_n(br, bs_nchunks(br.hi - br.lo));
+    // the slice kernel indexes a chunk's stream words in 32 bits (< 2^31: 3.4 M blocks
+    // per chunk, a 1.1e12-parameter stream at 512 chunks); longer chunks take the 19-seed kernel
+    for (int c = 0; C->have_bs && c < BP.nchunks; c++)
+      if ((BP.chunk_block[(size_t)c + 1] - BP.chunk_block[(size_t)c]) * kMtN >= ((int64_t)1 << 31)) C->have_bs = false;
+    if (!C->have_bs) BP = Plan{};
+  }
   const IrrChunks IC = irregular_chunks(L);
   std::vector<uint64_t> ipolys;
   if (C->have_irr) jump_polys_for_blocks(IC.lo, ipolys);

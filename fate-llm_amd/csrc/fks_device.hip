@@ -1386,56 +1386,45 @@ __global__ __launch_bounds__(kZrThreads) void fks_zreplay_kernel(ApplyArgs a) {
 }
 
 // ------------------------------------------------------------------ bf16 slice kernel
-// fks_apply_bs_kernel<MODE>: the bf16 fast segments of a reconstruct, 32 seeds per
-// pass, generator state BIT-SLICED (fks_bitslice.h).  One workgroup per CU, two
-// independent halves (chunks 2w and 2w+1 of the stream) sharing the LDS tables:
-//   * waves 0..4 of a half (pair waves): thread q < 312 owns Box-Muller pair q of every
-//     block; per block it reads state rows j1 and j1+8 (32 planes each), tempers their
-//     low bytes (temper_low8), transposes them to one byte per seed (transpose8), and
-//     runs the 32-seed update chain of its two parameters in order;
-//   * wave 5 of a half (twist wave) twists the half's state in place, block b -> b+1,
-//     while the pair waves run block b's chain: 10 rounds of 64 rows, all reads of a
-//     round before its writes (one wave: LDS operations complete in order).
-// Per block: barrier 1 (every pair wave holds block b's rows) -> twist || chain ->
-// barrier 2 (block b+1 is in place) -> the pair waves read + temper their rows.
-// (Replacing the two barriers by LDS flags -- each pair wave reading its rows as soon as
-// the twist rounds that write them are published, the halves drifting apart -- measured
-// 1-10 % SLOWER, and reading the next rows 4-16 seeds before the chain ends no faster:
-// profiles/r03b_ab_flags.log, r03d_ab_prefetch.log.)
-// LDS: [R f32 x 256 | (C,S) table | state half 0 | state half 1]; a half's state is 8
-// CHUNK arrays (planes 4q..4q+3 of all 624 rows, 16 B per row): consecutive rows are
-// consecutive 16 B, so the twist wave's row reads and writes are bank-conflict free; the
-// pair waves read row j1 first where (q >> 4) is even and row j1+8 first where it is
-// odd, which makes every 16-lane ds_read_b128 group hit 16 distinct rows mod 16.
+// fks_apply_bs_kernel<MODE>: the bf16 fast segments of a reconstruct, 32 seeds per pass,
+// generator state BIT-SLICED (fks_bitslice.h): row i of a chunk's state is state word i
+// of the 32 seeds as 32 bit planes.  One workgroup per CU holds the states of two chunks
+// (halves) in LDS; the work of a chunk is cut into TASKS of 128 consecutive stream words
+// (64 Box-Muller pairs: one wave), and the six waves of a half take the half's tasks
+// round-robin.  A wave runs the whole of its task:
+//   * twist: lane L owns the pair (j, j+8), j = 16 (L >> 3) + (L & 7) of the task, and
+//     twists exactly those two rows in place, block b -> b+1 (MT19937RNGEngine.h:164-175
+//     on 32 seeds at once): word u of the stream is f(word u-624 (plane 31 only: U31),
+//     word u-623 (V, the next slot), word u-227 (M));
+//   * the two new rows are still in registers: temper their low bytes (temper_low8),
+//     transpose them to one byte per seed, and run the 32-seed update chain of the lane's
+//     two parameters (thread owns Box-Muller pair (j, j+8): two table lookups, the z
+//     product and its rounding, the per-op-rounded update chain).
+// The twists of a half form one serial chain -- M of a task's last 29 words are words the
+// previous task wrote -- so a wave waits until the half's LDS flag counts n twisted
+// tasks, twists task n, and publishes n+1; the chains of different tasks overlap freely.
+// Against the round-2 form (five pair waves + one twist wave per half, two workgroup
+// barriers per MT block): no pair wave re-reads the rows the twist wave wrote (a quarter
+// of the LDS traffic), every wave carries the same instruction mix (no SIMD with three
+// pair waves beside one with the twist wave), no barrier per block; with that LDS time
+// freed, the (C,S) table is read as f32 pairs (one ds_read_b64, no unpack instructions):
+// 3.83 -> 3.39 ms per 32-seed launch over 2^28 params (profiles/r03s_ab.log; the
+// variants measured on the way are in profiles/r03k..r03s_ab.log).
+// LDS: [R f32 x 256 | (C,S) f32 pairs x 256 | state half 0 | state half 1 | 2 flags]; a
+// half's state is 8 CHUNK arrays (planes 4q..4q+3 of all 624 rows, 16 B per row), so a
+// row's chunk q is one ds_read_b128 / ds_write_b128.  The lane's first row is j+8 where
+// (L >> 3) is odd, which makes every 16-lane group of a ds_read_b128 (8-lane group of a
+// ds_write_b128) touch distinct rows mod 16: conflict free.
 constexpr int kBsChunkBytes = kMtN * 16;               // 9,984
 constexpr int kBsStateBytes = 8 * kBsChunkBytes;       // 79,872
-// (C,S): f32 pairs (8 B, ds_read_b64) or the two bf16 values packed in one dword (4 B,
-// ds_read_b32 + two unpack ops) for the chains without the weight-decay roundings
-// (kModeUpdateWd0 / NoWd: 3.84 vs 4.03 ms per launch, profiles/r02g_ab_wd0.log; a random
-// 8-bit-indexed ds_read_b64 costs 17.4 CU-cycles per wave-instruction against 6.5 for
-// ds_read_b32, tools/ubench/issue2.hip).  Planar C|S tables read by ds_read2st64_b32 or
-// two ds_read_b32 measured +19 % / +24 % (profiles/r02j_ab_planar.log, r02u_ab_planar2.log).
-constexpr int kBsCsBytes = 8;
-constexpr int kBsTabBytes = 256 * 4 + 256 * kBsCsBytes;  // 3,072
-template <int MODE>
-constexpr bool bs_cspack() {
-  return MODE == kModeUpdateWd0 || MODE == kModeUpdateNoWd;
-}
-constexpr int kBsLdsBytes = kBsTabBytes + 2 * kBsStateBytes;  // 162,816 <= 163,840
+constexpr int kBsTabBytes = 256 * 4 + 256 * 8;         // 3,072
+constexpr uint32_t kBsFlagOff = kBsTabBytes + 2 * kBsStateBytes;  // u32 twisted-task count per half
+constexpr int kBsLdsBytes = (int)kBsFlagOff + 8;       // 162,824 <= 163,840
 static_assert(kBsLdsBytes <= 163840, "slice kernel LDS");
-constexpr int kBsRounds = 10;                          // twist rounds of 64 rows per block
+constexpr int kBsWaves = kBsHalfThreads / 64;          // waves per half (6)
+constexpr int kBsTaskWords = 128;                      // stream words per task
 
 // the 32 planes of row i (row byte address ra = state base + 16 i)
-__device__ __forceinline__ void bs_load_row(uint32_t ra, uint32_t (&x)[32]) {
-#pragma unroll
-  for (int q = 0; q < 8; q++) {
-    const u32x4_t v = lds_u4(ra + q * kBsChunkBytes);
-    x[4 * q] = v.x;
-    x[4 * q + 1] = v.y;
-    x[4 * q + 2] = v.z;
-    x[4 * q + 3] = v.w;
-  }
-}
 __device__ __forceinline__ void bs_store_row(uint32_t ra, const uint32_t (&x)[32]) {
 #pragma unroll
   for (int q = 0; q < 8; q++) {
@@ -1444,51 +1433,18 @@ __device__ __forceinline__ void bs_store_row(uint32_t ra, const uint32_t (&x)[32
   }
 }
 
-// row addresses of twist round r for this lane: i = 64 r + lane; V = row i+1 (row 0 for
-// i = 623), M = row i+397 (i < 227) or i-227; lanes with i >= 624 read row 0 and do
-// not store.
-__device__ __forceinline__ void bs_round_rows(uint32_t sbase, int r, int lane, uint32_t& av, uint32_t& am) {
-  const int i = 64 * r + lane;
-  const int iv = i + 1 < kMtN ? i + 1 : 0;
-  const int im = i < kMtN - kMtM ? i + kMtM : (i < kMtN ? i - (kMtN - kMtM) : 0);
-  av = sbase + 16u * (uint32_t)iv;
-  am = sbase + 16u * (uint32_t)im;
+// The flag hand-off needs no memory fence: one wave's LDS operations are performed in
+// order, so a wave that reads the new count issues its row loads after the writer's row
+// stores were performed.  (A release fence would also wait for the writer's global
+// stores.)  The lgkmcnt(0) keeps the count from running ahead of stores still queued;
+// the asm barriers keep the compiler from moving LDS accesses across.
+__device__ __forceinline__ uint32_t bs_flag_load(uint32_t off) {
+  return *(volatile const lds_u32_t*)(size_t)off;
 }
-
-// The twist wave: the half's state, block b -> b+1, in place (MT19937RNGEngine.h:164-175
-// on 32 seeds at once).  Round r+1's reads are issued before round r's writes: they
-// touch rows i+1 >= 64(r+1) (not written before round r+1) and rows i+397 / i-227 of
-// earlier rounds only.  U31 (plane 31 of the old row i) is the V row of lane i-1: one
-// DPP wave_shr:1, lane 0 taking the previous round's lane 63.
-__device__ __forceinline__ void bs_twist_block(uint32_t sbase, int lane) {
-  uint32_t V[32], M[32];
-  uint32_t av, am;
-  // old row 0, plane 31 (every lane the same address: a broadcast read)
-  uint32_t prev63 = lds_u32((int)(sbase + 7 * kBsChunkBytes + 12));
-  bs_round_rows(sbase, 0, lane, av, am);
-  bs_load_row(av, V);
-  bs_load_row(am, M);
-#pragma unroll
-  for (int r = 0; r < kBsRounds; r++) {
-    uint32_t Vn[32], Mn[32];
-    if (r + 1 < kBsRounds) {
-      uint32_t avn, amn;
-      bs_round_rows(sbase, r + 1, lane, avn, amn);
-      bs_load_row(avn, Vn);
-      bs_load_row(amn, Mn);
-    }
-    const uint32_t u31 = (uint32_t)__builtin_amdgcn_update_dpp((int)prev63, (int)V[31], 0x138, 0xF, 0xF, false);
-    prev63 = (uint32_t)__builtin_amdgcn_readlane((int)V[31], 63);
-    bs::twist_row_inplace(V, M, u31);  // M now holds the new row i
-    if (r < kBsRounds - 1 || 64 * r + lane < kMtN) bs_store_row(sbase + 16u * (uint32_t)(64 * r + lane), M);
-    if (r + 1 < kBsRounds) {
-#pragma unroll
-      for (int b = 0; b < 32; b++) {
-        V[b] = Vn[b];
-        M[b] = Mn[b];
-      }
-    }
-  }
+__device__ __forceinline__ void bs_flag_store(uint32_t off, uint32_t v) {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  *(volatile lds_u32_t*)(size_t)off = v;
 }
 
 // byte c of w times 2^S with a compile-time c (SDWA)
@@ -1510,29 +1466,20 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   const int lane = tid & 63;
   const int half = __builtin_amdgcn_readfirstlane(tid >= kBsHalfThreads ? 1 : 0);
   const int ht = tid - half * kBsHalfThreads;
-  // waves 0..4 of a half pair waves, 5 the twist wave: waves w, w+4, w+8 share a SIMD
-  // (profiles/r02f_simdmap.log), so the twist waves 5 and 11 sit on SIMDs 1 and 3
-  // (both on one SIMD measured +5 %, profiles/r02i_ab_rolemap.log)
   const int hw = __builtin_amdgcn_readfirstlane(ht >> 6);
   const int c = kBsChunksPerWg * (int)blockIdx.x + half;
   const int nseeds = FULL ? kBsSeeds : a.nseeds;
   const int64_t b0 = a.chunk_block[c], b1 = a.chunk_block[c + 1];
-  const int64_t w0 = a.chunk_block[kBsChunksPerWg * blockIdx.x];
-  const int64_t wm = a.chunk_block[kBsChunksPerWg * blockIdx.x + 1];
-  const int64_t w1 = a.chunk_block[kBsChunksPerWg * blockIdx.x + 2];
-  const int64_t nb = (wm - w0) > (w1 - wm) ? (wm - w0) : (w1 - wm);  // iterations (both halves)
-  const int64_t mynb = b1 - b0;
+  const int nwords = (int)(kMtN * (b1 - b0));  // < 2^31 (launch_apply_bs checks the chunk table's bound)
+  const int ntask = (nwords + kBsTaskWords - 1) / kBsTaskWords;
   const uint32_t sbase = kBsTabBytes + (uint32_t)half * kBsStateBytes;
+  const uint32_t flag = kBsFlagOff + 4u * (uint32_t)half;
 
   for (int i = tid; i < 256; i += kBsThreads) {
     reinterpret_cast<float*>((uint8_t*)lds32)[i] = c_tab_bf16[i];
-    if (bs_cspack<MODE>())  // C in the low half, S in the high half (both exact bf16 values)
-      reinterpret_cast<uint32_t*>((uint8_t*)lds32 + 1024)[i] =
-          (__float_as_uint(c_tab_bf16[256 + i]) >> 16) | (__float_as_uint(c_tab_bf16[512 + i]) & 0xffff0000u);
-    else
-      reinterpret_cast<float2*>((uint8_t*)lds32 + 1024)[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
+    reinterpret_cast<float2*>((uint8_t*)lds32 + 1024)[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
   }
-  // prologue: the jump windows of this chunk, transposed into planes
+  // prologue: the jump windows of this chunk (the state before block b0), as planes
   for (int i = ht; i < kMtN; i += kBsHalfThreads) {
     uint32_t w[32];
 #pragma unroll
@@ -1540,40 +1487,22 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
     bs::transpose32(w);
     bs_store_row(sbase + 16u * (uint32_t)i, w);
   }
-  __syncthreads();
-  // The twist wave and the pair waves run separate loops with the same barrier
-  // sequence (s_barrier is workgroup-wide whatever the program counter), so the
-  // twist's 4 x 32 row registers are never live together with the pair state.
-  if (hw == 5) {
-    if (mynb > 0) bs_twist_block(sbase, lane);  // -> block b0
-    __syncthreads();                              // state holds block b0
-    for (int64_t t = 0; t < nb; t++) {
-      __syncthreads();                            // every pair wave holds its rows of block b
-      if (t + 1 < mynb) bs_twist_block(sbase, lane);  // -> block b + 1
-      __syncthreads();
-    }
-    return;
-  }
+  if (ht == 0) lds32[flag / 4] = 0u;
+  __syncthreads();  // the only workgroup barrier
 
-  // pair lanes (waves 0..4 of the half)
-  const int q = ht < kMtN / 2 ? ht : kMtN / 2 - 1;
-  const bool lane_on = ht < kMtN / 2;
-  const int j1 = 16 * (q >> 3) + (q & 7);
-  const bool flip = ((q >> 4) & 1) != 0;
-  const uint32_t ra_first = sbase + 16u * (uint32_t)(flip ? j1 + 8 : j1);
-  const uint32_t ra_second = sbase + 16u * (uint32_t)(flip ? j1 : j1 + 8);
+  const int toff = 16 * (lane >> 3) + (lane & 7);  // the lane's words toff, toff + 8 of a task
+  const bool flip = ((lane >> 3) & 1) != 0;
+  const bool odd = (lane & 1) != 0;
 
   float gk[kBsSeeds];
 #pragma unroll
   for (int k = 0; k < kBsSeeds; k++) gk[k] = a.g[k];
-  // the pair waves issue first on the two SIMDs that also hold a twist wave (measured
-  // 6 % faster per launch; the twist wave first instead: 5 % slower)
-  __builtin_amdgcn_s_setprio(1);
 
   // the lane's current segment (positions only grow)
+  const int64_t wbase = (int64_t)kMtN * b0;  // stream position of the chunk's first word
   int cur;
   {
-    const int64_t s1 = (int64_t)kMtN * b0 + j1;
+    const int64_t s1 = wbase + (int64_t)kBsTaskWords * hw + toff;
     int lo = 0, hi = a.nsegs;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
@@ -1601,96 +1530,147 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   };
   load_seg();
 
-  const bool odd = (tid & 1) != 0;
+  // The lane's parameters of task n: elements toff, toff + 8 of the task, loaded as the
+  // aligned pairs (j, j+1) (even lane j) and (j+7, j+8) (odd lane j+1) and exchanged with
+  // the neighbour lane (swap_adjacent).  Lanes past the chunk or off every fast segment
+  // read and write the sink.
   using ST = Traits<MODE == kModeDelta ? FKS_F32 : FKS_BF16>;
   constexpr int kEs = MODE == kModeDelta ? 4 : 2;
   typedef typename ST::Pair Pair;
   struct Slot { uint64_t addr; float lr, wd; uint32_t wdf; Pair raw; };
-  auto fetch = [&](int64_t b) -> Slot {
+  auto fetch = [&](int n) -> Slot {
     Slot sl;
-    const int64_t s1 = (int64_t)kMtN * b + j1;
+    const int u1 = kBsTaskWords * n + toff;
+    const int64_t s1 = wbase + u1;
     while (s1 >= seg_end) { cur++; load_seg(); }
-    const bool on = lane_on && s1 >= seg_start;
+    const bool on = u1 < nwords && s1 >= seg_start;
     sl.lr = seg_lr; sl.wd = seg_wd; sl.wdf = seg_wdf;
     sl.addr = on ? seg_ptr + (uint64_t)(s1 - seg_start + (odd ? 7 : 0)) * kEs : (uint64_t)(uintptr_t)a.sink;
     sl.raw = ST::load_pair(sl.addr);
     return sl;
   };
-  Slot sl = fetch(b0);
-  *reinterpret_cast<volatile uint32_t*>(a.sink + 1) = 0u;
-  __syncthreads();  // state holds block b0
 
-  // rows j1 and j1 + 8 of the state -> the lane's tempered radius / angle bytes, 8 planes
-  // each (transposed to one byte per seed right before use)
-  uint32_t oa[8], ob[8];
-  auto read_rows = [&]() {
-    uint32_t x1[32], x2[32];
-    bs_load_row(ra_first, x1);  // (the last block re-reads rows it does not use)
-    bs_load_row(ra_second, x2);
+  // ---- the twist of task n: the lane's two rows in place; returns the tempered radius
+  // bytes (row toff) and angle bytes (row toff + 8) as planes.  Streamed over the 8 chunk
+  // arrays (planes 4q..4q+3): chunk q of every row of the task is loaded (V, M) before
+  // any lane stores it -- through data dependence, since new plane 4q+3 needs V plane
+  // 4q+4 of chunk q+1, loaded one step ahead; U31 and V plane 0 are loaded first.  M rows
+  // lie 227 words back, outside the task, so the task never stores them.
+  auto twist = [&](const int n, uint32_t (&oa)[8], uint32_t (&ob)[8]) {
+    const int u1 = kBsTaskWords * n + toff;
+    const bool valid = u1 < nwords;
+    const int i1 = valid ? u1 % kMtN : 0;
+    const int ia = flip ? i1 + 8 : i1, ib = flip ? i1 : i1 + 8;  // first / second row
+    auto rows = [&](int i, uint32_t& av, uint32_t& am, uint32_t& au) {
+      const int iv = i + 1 < kMtN ? i + 1 : 0;
+      const int im = i < kMtN - kMtM ? i + kMtM : i - (kMtN - kMtM);
+      av = sbase + 16u * (uint32_t)iv;
+      am = sbase + 16u * (uint32_t)im;
+      au = sbase + 7u * kBsChunkBytes + 16u * (uint32_t)i + 12u;
+    };
+    uint32_t av1, am1, au1, av2, am2, au2;
+    rows(ia, av1, am1, au1);
+    rows(ib, av2, am2, au2);
+    uint32_t M1[32], M2[32];  // the new rows
+    const uint32_t U1 = lds_u32((int)au1), U2 = lds_u32((int)au2);
+    u32x4_t va = lds_u4(av1), vb = lds_u4(av2), ma = lds_u4(am1), mb = lds_u4(am2);
+    const uint32_t v0a = va.x, v0b = vb.x;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      u32x4_t va2 = va, vb2 = vb, ma2 = ma, mb2 = mb;
+      if (q < 7) {
+        va2 = lds_u4(av1 + (q + 1) * kBsChunkBytes);
+        vb2 = lds_u4(av2 + (q + 1) * kBsChunkBytes);
+        ma2 = lds_u4(am1 + (q + 1) * kBsChunkBytes);
+        mb2 = lds_u4(am2 + (q + 1) * kBsChunkBytes);
+      }
+      const uint32_t Va[5] = {va.x, va.y, va.z, va.w, va2.x};
+      const uint32_t Vb[5] = {vb.x, vb.y, vb.z, vb.w, vb2.x};
+      const uint32_t Ma[4] = {ma.x, ma.y, ma.z, ma.w}, Mb[4] = {mb.x, mb.y, mb.z, mb.w};
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        // bs::twist_row plane by plane: plane b of y >> 1 is V plane b+1 (b < 30; t = 3
+        // reads chunk q+1's plane 0), U31 (b = 30), none (b = 31)
+        const int b = 4 * q + t;
+        const bool am = ((bs::kMatrixA >> b) & 1u) != 0;
+        uint32_t xa, xb;
+        if (b < 30) { xa = Va[t + 1]; xb = Vb[t + 1]; }
+        else if (b == 30) { xa = U1; xb = U2; }
+        else { xa = 0u; xb = 0u; }
+        M1[b] = am ? bs::xor3(Ma[t], xa, v0a) : (Ma[t] ^ xa);
+        M2[b] = am ? bs::xor3(Mb[t], xb, v0b) : (Mb[t] ^ xb);
+      }
+      if (valid) {
+        lds_st4(sbase + 16u * (uint32_t)ia + q * kBsChunkBytes, u32x4_t{M1[4 * q], M1[4 * q + 1], M1[4 * q + 2], M1[4 * q + 3]});
+        lds_st4(sbase + 16u * (uint32_t)ib + q * kBsChunkBytes, u32x4_t{M2[4 * q], M2[4 * q + 1], M2[4 * q + 2], M2[4 * q + 3]});
+      }
+      va = va2; vb = vb2; ma = ma2; mb = mb2;
+    }
     uint32_t o1[8], o2[8];
-    bs::temper_low8(x1, o1);
-    bs::temper_low8(x2, o2);
+    bs::temper_low8(M1, o1);
+    bs::temper_low8(M2, o2);
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-      oa[j] = flip ? o2[j] : o1[j];  // row j1: the radius uniforms
-      ob[j] = flip ? o1[j] : o2[j];  // row j1 + 8: the angle uniforms
+      oa[j] = flip ? o2[j] : o1[j];  // row toff: the radius uniforms
+      ob[j] = flip ? o1[j] : o2[j];  // row toff + 8: the angle uniforms
     }
   };
-  // seed k's table lookups (R[a], (C,S)[b]) and its step of the update chain
-  auto lookup = [&](int k, f32x2_t& rr, f32x2_t& cs) {
-    const uint32_t ia = bs_index<2>(oa[k & 7], k >> 3);
-    const uint32_t ib = bs_index<bs_cspack<MODE>() ? 2 : 3>(ob[k & 7], k >> 3);
-    const float r = lds_f32(ia);
-    rr = f32x2_t{r, r};
-    if (bs_cspack<MODE>()) {
-      const uint32_t w = lds_u32((int)(1024u + ib));
-      cs = f32x2_t{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
-    } else {
-      cs = lds_f32x2(1024u + ib);
-    }
-  };
-  auto chain = [&](int k, f32x2_t p, f32x2_t rr, f32x2_t cs) -> f32x2_t {
-    const f32x2_t zero = {0.0f, 0.0f};
-    const f32x2_t z = rnd2<FKS_BF16>(__builtin_elementwise_fma(rr, cs, zero));
-    return apply_pair<FKS_BF16, MODE>(p, z, gk[k], sl.lr, sl.wd, sl.wdf != 0, 0.0f);
-  };
-  if (mynb > 0) read_rows();
 
-  for (int64_t t = 0; t < nb; t++) {
-    const bool act = t < mynb;  // half-uniform
-    const int64_t b = b0 + t;
-    __syncthreads();  // barrier 1: every pair wave holds block b's rows; the twist starts block b+1
-    if (act) {
-      const Slot nxt = fetch(b + 1 < b1 ? b + 1 : b);
-      bs::transpose8(oa);
-      bs::transpose8(ob);
-      f32x2_t p;
-      {
-        const uint32_t keep = odd ? ST::hi(sl.raw) : ST::lo(sl.raw);
-        const uint32_t got = swap_adjacent(odd ? ST::lo(sl.raw) : ST::hi(sl.raw));
-        p.x = ST::cvt(odd ? got : keep);
-        p.y = ST::cvt(odd ? keep : got);
-      }
-#pragma unroll
-      for (int k = 0; k < kBsSeeds; k++) {
-        if (FULL || k < nseeds) {
-          f32x2_t rr, cs;
-          lookup(k, rr, cs);
-          p = chain(k, p, rr, cs);
-        }
-        // the lookups of one byte column (8 seeds) at a time: hoisting all 64 table
-        // reads ahead of the chain would spill (pinned lookaheads of 1-8 seeds measured
-        // -0.3..+6.7 %, profiles/r02f_ab_la.log)
-        if ((k % kBsFence) == kBsFence - 1) asm volatile("" ::: "memory");
-      }
-      const uint32_t b1v = ST::bits(p.x), b2v = ST::bits(p.y);
-      const uint32_t back = swap_adjacent(odd ? b1v : b2v);
-      const Pair out = odd ? ST::pack(back, b2v) : ST::pack(b1v, back);
-      ST::store_pair(sl.addr, out);
-      sl = nxt;
+  // ---- the 32-seed chain of the lane's two parameters (slot sl), z from the bytes of
+  // twist(): z = bf16(R[a] C[b]) + 0, bf16(R[a] S[b]) + 0 (normal_fill_16<BFloat16>: an
+  // exact f32 product, one rounding; the fma's +0 turns -0 into +0 like "+ mean")
+  auto chain = [&](const Slot& sl, uint32_t (&oa)[8], uint32_t (&ob)[8]) {
+    bs::transpose8(oa);
+    bs::transpose8(ob);
+    f32x2_t p;
+    {
+      const uint32_t keep = odd ? ST::hi(sl.raw) : ST::lo(sl.raw);
+      const uint32_t got = swap_adjacent(odd ? ST::lo(sl.raw) : ST::hi(sl.raw));
+      p.x = ST::cvt(odd ? got : keep);
+      p.y = ST::cvt(odd ? keep : got);
     }
-    __syncthreads();  // barrier 2: the twist of block b + 1 is in place
-    read_rows();
+#pragma unroll
+    for (int k = 0; k < kBsSeeds; k++) {
+      if (FULL || k < nseeds) {
+        const float r = lds_f32(bs_index<2>(oa[k & 7], k >> 3));
+        const f32x2_t rr = {r, r}, zero = {0.0f, 0.0f};
+        const f32x2_t cs = lds_f32x2(1024u + bs_index<3>(ob[k & 7], k >> 3));
+        const f32x2_t z = rnd2<FKS_BF16>(__builtin_elementwise_fma(rr, cs, zero));
+        p = apply_pair<FKS_BF16, MODE>(p, z, gk[k], sl.lr, sl.wd, sl.wdf != 0, 0.0f);
+      }
+      // the lookups of one byte column (8 seeds) at a time: hoisting all 64 table reads
+      // ahead of the chain would spill
+      if ((k % kBsFence) == kBsFence - 1) asm volatile("" ::: "memory");
+    }
+    const uint32_t b1v = ST::bits(p.x), b2v = ST::bits(p.y);
+    const uint32_t back = swap_adjacent(odd ? b1v : b2v);
+    const Pair out = odd ? ST::pack(back, b2v) : ST::pack(b1v, back);
+    ST::store_pair(sl.addr, out);
+  };
+
+  // ---- task n: wait for task n-1's twist, twist, publish, chain; fetches task n + 6
+  // into nx (past the last task: the sink)
+  auto task = [&](const int n, const Slot& sl, Slot& nx) {
+    uint32_t oa[8], ob[8];
+    __builtin_amdgcn_s_setprio(2);
+    while (__builtin_amdgcn_readfirstlane(bs_flag_load(flag)) < (uint32_t)n) __builtin_amdgcn_s_sleep(0);
+    asm volatile("" ::: "memory");
+    twist(n, oa, ob);
+    if (lane == 0) bs_flag_store(flag, (uint32_t)n + 1u);
+    __builtin_amdgcn_s_setprio(0);
+    nx = fetch(n + kBsWaves);
+    chain(sl, oa, ob);
+  };
+
+  // two named slots and a loop unrolled by two: a slot copy on the back edge would wait
+  // for the load -- and the store before it -- at the top of every task
+  if (hw >= ntask) return;
+  Slot s0 = fetch(hw), s1;
+  for (int n = hw;;) {
+    task(n, s0, s1);
+    if ((n += kBsWaves) >= ntask) break;
+    task(n, s1, s0);
+    if ((n += kBsWaves) >= ntask) break;
   }
 }
 

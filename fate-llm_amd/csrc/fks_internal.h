@@ -151,8 +151,9 @@ struct IrrArgs {
 };
 
 // bf16 slice kernel (fks_apply_bs_kernel): 32 seeds per pass, bit-sliced generator
-// state; one workgroup per CU holds two chunks (two 384-thread halves: 5 Box-Muller
-// pair waves + 1 twist wave each) and LDS = 3 KB of tables + 2 x 79,872 B of state.
+// state; one workgroup per CU holds two chunks (two 384-thread halves of six waves, each
+// wave twisting and updating 128-word tasks of its chunk) and LDS = 3 KB of tables +
+// 2 x 79,872 B of state + two task flags.
 constexpr int kBsSeeds = 32;
 constexpr int kBsHalfThreads = 384;
 constexpr int kBsThreads = 2 * kBsHalfThreads;
