@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--params", type=int, default=0)
     ap.add_argument("--ks", default="1,19,304,4096")
     ap.add_argument("--hd-k", type=int, default=4096)
+    ap.add_argument("--wd", type=lambda v: None if v == "none" else float(v), default=0.0,
+                    help="weight decay (default 0.0, bench.py's: the HF default the reference passes)")
     args = ap.parse_args()
     from fate_llm.algo.fedkseed import codec
 
@@ -45,7 +47,7 @@ def main():
     for s in shapes:
         views.append(flat[off:off + bench.numel(s)])
         off += bench.numel(s)
-    specs = [codec.ParamSpec(v, lr=1e-5, weight_decay=0.01) for v in views]
+    specs = [codec.ParamSpec(v, lr=1e-5, weight_decay=args.wd) for v in views]
     seeds, scalars = bench.synthetic_seeds(max(max(int(k) for k in args.ks.split(",")), args.hd_k))
     out = {"params": total, "bytes": total * 2}
 
@@ -73,7 +75,7 @@ def main():
         kv = [g for g in scalars[:args.hd_k] if g != 0.0]
         t_rec = timed(lambda: codec.directional_step(specs, ks, kv))
     t_d2h = timed(lambda: host.copy_(flat, non_blocking=True))
-    out.update({"k": args.hd_k, "h2d_s": round(t_h2d, 4), "h2d_GBps": round(total * 2 / t_h2d / 1e9, 2),
+    out.update({"k": args.hd_k, "weight_decay": args.wd, "h2d_s": round(t_h2d, 4), "h2d_GBps": round(total * 2 / t_h2d / 1e9, 2),
                 "reconstruct_s": round(t_rec, 3), "d2h_s": round(t_d2h, 4),
                 "d2h_GBps": round(total * 2 / t_d2h / 1e9, 2), "d2h_first_s": round(t_d2h0, 4),
                 "device_resident_GBps": round(total * 2 / t_rec / 1e9, 4),
