@@ -63,7 +63,7 @@ VALU_MIX_CYCLES = 4.43
 VALU_MIX_CEILING_TLANEOPS = 1024 * 64 * 2.4e9 / VALU_MIX_CYCLES / 1e12
 # per-launch counters of the bf16 slice kernel (fks_apply_bs_kernel), tools/summarize_pmc2.py: the
 # weight-decay chain (wd != 0) and the zero-weight-decay chain (kModeUpdateWd0)
-PMC_SUMMARIES = {"wd": "pmc_apply_r03b_full.json", "wd0": "pmc_apply_r03b_wd0.json"}
+PMC_SUMMARIES = {"wd": "pmc_apply_r03c_full.json", "wd0": "pmc_apply_r03c_wd0.json"}
 
 
 def llama7b_shapes():
@@ -367,7 +367,7 @@ def run(args, world, rank, local):
     value = buf_bytes / (dt / args.steps) / 1e9
 
     # ---- rooflines of the dominant kernel, this rank: the bf16 slice kernel
-    # (fks_apply_bs_kernel, 32 seeds per launch) for every reconstruct of >= 20 seeds
+    # (fks_apply_bs_kernel, 64 seeds per launch) for every reconstruct of >= 20 seeds
     n_steps_prof = args.steps + args.warmup
     rank_params = total if seed_shard else (shard_words[rank % nshards][1] - shard_words[rank % nshards][0])
     n_apply = max(prof.n_apply, 1)
@@ -411,7 +411,7 @@ def run(args, world, rank, local):
                              "wave-instruction (profiles/r02_ubench_issue3.log)")}
     # the north star's roof: algorithmic HBM bytes of the WHOLE reconstruct (read + write the
     # buffer once, SURVEY.md §8(d): 2 N elt) over the reconstruct time; the per-pass figure
-    # (each 32-seed launch streams its shard once) is reported beside it, named as such
+    # (each 64-seed launch streams its shard once) is reported beside it, named as such
     elt = 4 if seed_shard else 2
     alg_bytes_step = 2 * total * 2 * (world if weak else 1)
     hbm_ach = alg_bytes_step / (dt / args.steps) / 1e9 / world  # per GPU, against one GPU's peak
@@ -422,7 +422,7 @@ def run(args, world, rank, local):
            "alg_bytes_per_step": alg_bytes_step,
            "per_pass": {"alg_bytes_per_launch": 2 * rank_params * elt,
                         "achieved_GBps": round(2 * rank_params * elt / avg_apply_s / 1e9, 2),
-                        "note": "one launch reads + writes its shard once (32 seeds); a reconstruct is "
+                        "note": f"one launch reads + writes its shard once ({round(seeds_per_launch)} seeds); a reconstruct is "
                                 f"{round(n_apply / n_steps_prof)} such passes"}}
     out = {
         "metric": "GB/s param buffer reconstructed from (seed,scalar) list, device-resident",

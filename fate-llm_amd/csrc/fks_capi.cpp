@@ -365,7 +365,8 @@ size_t ws_bytes_for(int chunks, int seeds_per_pass) {
   return kWsStatesOff + sizeof(uint32_t) * kMtN * (size_t)seeds_per_pass * (size_t)std::max(chunks, 1);
 }
 
-// the slice kernel's plan: kBsChunksPerWg chunks per workgroup, one workgroup per CU
+// the slice kernel's plan: two chunks per workgroup, one workgroup per CU (a pass of
+// > 32 seeds runs two seed slices on each chunk PAIR, a pass of <= 32 one slice per chunk)
 int bs_nchunks(int64_t nblocks) {
   const int64_t wgs = std::max<int64_t>(1, std::min<int64_t>(device_cu_count(), (nblocks + 1) / 2));
   return (int)(kBsChunksPerWg * wgs);
@@ -462,6 +463,7 @@ struct CachedPlan {
   int wd_mode[3] = {kModeUpdate, kModeUpdate, kModeUpdate};  // kModeUpdateWd / NoWd when uniform
   bool have_reg = false, have_irr = false;
   bool have_bs = false;  // bf16 fast segments with their slice-kernel plan (non-small calls)
+  int64_t bs_blocks = 0; // MT blocks the slice-kernel plan covers
   uint64_t chunk_hash = 0;  // the chunk starts (regular + irregular): what a seed's windows depend on
   int64_t reg_lo = 0, reg_hi = 0;  // MT blocks [reg_lo, reg_hi) the regular chunks cover
   uint64_t bf16_hash = 0;  // the bf16 segments' stream ranges: which blocks a z-index store covers
@@ -567,10 +569,12 @@ CachedPlan* build_plan(const fks_tensor* t, int nt, const double* scales, uint64
   C->have_bs = !small && !L.segs[FKS_BF16].empty();
   if (C->have_bs) {
     BP = make_plan_n(br, bs_nchunks(br.hi - br.lo));
+    C->bs_blocks = br.hi - br.lo;
     // the slice kernel indexes a chunk's stream words in 32 bits (< 2^31: 3.4 M blocks
-    // per chunk, a 1.1e12-parameter stream at 512 chunks); longer chunks take the 19-seed kernel
+    // per plan chunk pair, a 5.6e11-parameter stream at 512 chunks); longer chunks take the 19-seed kernel
     for (int c = 0; C->have_bs && c < BP.nchunks; c++)
-      if ((BP.chunk_block[(size_t)c + 1] - BP.chunk_block[(size_t)c]) * kMtN >= ((int64_t)1 << 31)) C->have_bs = false;
+      if ((BP.chunk_block[(size_t)std::min(c + 2, BP.nchunks)] - BP.chunk_block[(size_t)c]) * kMtN >= ((int64_t)1 << 31))
+        C->have_bs = false;
     if (!C->have_bs) BP = Plan{};
   }
   const IrrChunks IC = irregular_chunks(L);
@@ -884,7 +888,7 @@ PhxPlan* get_phx_plan(const fks_tensor* t, int nt, const double* scales) {
   return P;
 }
 
-// the torch_rocm stream: seeds in passes of kBsSeeds (by value in the kernel arguments);
+// the torch_rocm stream: seeds in passes of kPhxSeeds (by value in the kernel arguments);
 // element shards split the work items
 void run_philox(const fks_tensor* t, int nt, const uint64_t* seeds, const double* values, int k, int value_kind,
                 int mode, void* stream, const double* scales, int shard, int nshards, const float* gdev) {
@@ -937,6 +941,7 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
   // 19-seed pass go to the bit-sliced slice kernel, 32 seeds per pass
   const bool use_bs = C->have_bs && k >= kBsMinSeeds && (mode == kModeUpdate || mode == kModeDelta);
   size_t need = ws_bytes_for(std::max(C->Z.reg_chunks, C->Z.irr_chunks), std::min(per_pass, k));
+  // (a slice pass holds <= 64 seeds x half the plan chunks, a split pass <= 32 x all of them)
   if (use_bs) need = std::max(need, ws_bytes_for(C->Z.bs_chunks, std::min(kBsSeeds, k)));
   if (!workspace || ws_bytes < need)
     throw Error(-FKS_EINVAL, "workspace too small: need " + std::to_string(need) + " bytes, got " +
@@ -1005,15 +1010,29 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
     return value_kind == FKS_VALUE_TENSOR ? round_to_dtype(values[s], d) : (float)values[s];
   };
   if (use_bs) {
-    for (int s0 = 0; s0 < k; s0 += kBsSeeds) {
-      const int nb = std::min(kBsSeeds, k - s0);
+    // Passes of 64 seeds as two slices per chunk pair (one jump per seed and chunk PAIR)
+    // or of 32 seeds, one slice per plan chunk (a serial twist chain half as long per
+    // chunk).  Per seed: two slices 0.395 ps per parameter + 36 us of jumps, one slice
+    // 0.387 ps + 71 us (profiles/r03w_ab.log, r03b/r03c bench lines): two slices pay
+    // below 4e9 parameters (every element shard of a multi-GPU 7B, the smaller models),
+    // one slice above (a whole 7B buffer).  FKS_BS_SLICES=1|2 forces one (diagnostics).
+    int slices = (C->Z.bs_chunks > 0 && (double)(kMtN * (double)C->bs_blocks) < 4e9) ? 2 : 1;
+    if (const char* e = std::getenv("FKS_BS_SLICES")) slices = (e[0] == '1') ? 1 : (e[0] == '2') ? 2 : slices;
+    const int per_pass = slices == 2 ? kBsPassSeeds : kBsSeeds;
+    for (int s0 = 0; s0 < k; s0 += per_pass) {
+      const int nb = std::min(per_pass, k - s0);
+      // > 32 seeds: two slices per chunk pair (jumps to every other plan boundary);
+      // <= 32: one slice per plan chunk
+      const bool split = nb <= kBsSeeds;
+      const int nch = split ? C->Z.bs_chunks : C->Z.bs_chunks / kBsChunksPerWg;
       JumpArgs ja{};
       for (int j = 0; j < nb; j++) ja.seeds[j] = seeds[s0 + j];
       ja.polys = reinterpret_cast<const uint64_t*>(hdr + C->H.off_bs_polys);
       ja.chunk_block = reinterpret_cast<const int64_t*>(hdr + C->H.off_bs_cb);
       ja.states = states;
-      ja.nchunks = C->Z.bs_chunks;
-      ja.chunks_per_wg = std::max(1, std::min(nb * C->Z.bs_chunks >= 4096 ? 32 : 16, C->Z.bs_chunks));
+      ja.nchunks = nch;
+      ja.stride = split ? 1 : kBsChunksPerWg;
+      ja.chunks_per_wg = std::max(1, std::min(nb * nch >= 4096 ? 32 : 16, nch));
       check(timed(1, stream, [&] { return launch_jump(ja, nb, stream); }), "fks_jump_kernel");
       ApplyBsArgs ba{};
       ba.states = states;
@@ -1022,7 +1041,8 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
       ba.chunk_block = ja.chunk_block;
       ba.sink = reinterpret_cast<uint64_t*>(ws);
       ba.nsegs = C->nsegs[FKS_BF16];
-      ba.nchunks = C->Z.bs_chunks;
+      ba.nchunks = nch;
+      ba.split = split ? 1 : 0;
       ba.nseeds = nb;
       ba.mode = mode == kModeUpdate ? C->wd_mode[FKS_BF16] : mode;
       check(timed(0, stream, [&] { return launch_apply_bs(ba, stream); }), "fks_apply_bs_kernel");

@@ -299,7 +299,8 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
   const int c0 = blockIdx.y * a.chunks_per_wg;
   const int c1 = min(c0 + a.chunks_per_wg, a.nchunks);
   for (int c = c0 + wave; c < c1; c += kJumpThreads / 64) {
-    const int64_t b = a.chunk_block[c];
+    const int st = a.stride > 0 ? a.stride : 1;
+    const int64_t b = a.chunk_block[(size_t)c * st];
     uint32_t acc[kW];
 #pragma unroll
     for (int j = 0; j < kW; j++) acc[j] = 0u;
@@ -308,7 +309,7 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
 #pragma unroll
         for (int j = 0; j < kW; j++) acc[j] = kW * lane + j < kMtN ? xs[kW * lane + j] : 0u;
       } else {
-        const uint64_t* poly = a.polys + (size_t)c * 312;  // wave-uniform: scalar loads
+        const uint64_t* poly = a.polys + (size_t)c * st * 312;  // wave-uniform: scalar loads
         uint32_t win[16];
         {
           const uint4 q0 = lds_b64x2(yb), q1 = lds_b64x2(yb + 4), q2 = lds_b64x2(yb + 8), q3 = lds_b64x2(yb + 12);
@@ -1386,12 +1387,12 @@ __global__ __launch_bounds__(kZrThreads) void fks_zreplay_kernel(ApplyArgs a) {
 }
 
 // ------------------------------------------------------------------ bf16 slice kernel
-// fks_apply_bs_kernel<MODE>: the bf16 fast segments of a reconstruct, 32 seeds per pass,
-// generator state BIT-SLICED (fks_bitslice.h): row i of a chunk's state is state word i
-// of the 32 seeds as 32 bit planes.  One workgroup per CU holds the states of two chunks
-// (halves) in LDS; the work of a chunk is cut into TASKS of 128 consecutive stream words
-// (64 Box-Muller pairs: one wave), and the six waves of a half take the half's tasks
-// round-robin.  A wave runs the whole of its task:
+// fks_apply_bs_kernel<MODE>: the bf16 fast segments of a reconstruct, 64 seeds per pass
+// as two SLICES of 32, generator state BIT-SLICED (fks_bitslice.h): row i of a slice's
+// state is state word i of its 32 seeds as 32 bit planes.  One workgroup per CU takes one
+// chunk and holds both slices' states in LDS, one per half.  The work of a chunk is cut
+// into TASKS of 128 consecutive stream words (64 Box-Muller pairs: one wave), and the six
+// waves of a half take the half's tasks round-robin.  A wave runs the whole of its task:
 //   * twist: lane L owns the pair (j, j+8), j = 16 (L >> 3) + (L & 7) of the task, and
 //     twists exactly those two rows in place, block b -> b+1 (MT19937RNGEngine.h:164-175
 //     on 32 seeds at once): word u of the stream is f(word u-624 (plane 31 only: U31),
@@ -1403,6 +1404,12 @@ __global__ __launch_bounds__(kZrThreads) void fks_zreplay_kernel(ApplyArgs a) {
 // The twists of a half form one serial chain -- M of a task's last 29 words are words the
 // previous task wrote -- so a wave waits until the half's LDS flag counts n twisted
 // tasks, twists task n, and publishes n+1; the chains of different tasks overlap freely.
+// Half 1 applies its seeds to what half 0 stored: its wave for task n waits until the
+// half-0 wave of task n+6 has published that store as complete before it prefetches
+// task n+6's parameters (half 0 publishes task m at its task m+6, after s_waitcnt
+// vmcnt(0): workgroup-scope release; half 0 never waits for half 1).  Two slices per
+// workgroup instead of two chunks halve the jumps (one per seed and chunk) and the HBM
+// passes of a reconstruct.
 // Against the round-2 form (five pair waves + one twist wave per half, two workgroup
 // barriers per MT block): no pair wave re-reads the rows the twist wave wrote (a quarter
 // of the LDS traffic), every wave carries the same instruction mix (no SIMD with three
@@ -1410,7 +1417,8 @@ __global__ __launch_bounds__(kZrThreads) void fks_zreplay_kernel(ApplyArgs a) {
 // freed, the (C,S) table is read as f32 pairs (one ds_read_b64, no unpack instructions):
 // 3.83 -> 3.39 ms per 32-seed launch over 2^28 params (profiles/r03s_ab.log; the
 // variants measured on the way are in profiles/r03k..r03s_ab.log).
-// LDS: [R f32 x 256 | (C,S) f32 pairs x 256 | state half 0 | state half 1 | 2 flags]; a
+// LDS: [R f32 x 256 | (C,S) f32 pairs x 256 | state half 0 | state half 1 | 2 twist flags |
+// 6 half-0 progress words]; a
 // half's state is 8 CHUNK arrays (planes 4q..4q+3 of all 624 rows, 16 B per row), so a
 // row's chunk q is one ds_read_b128 / ds_write_b128.  The lane's first row is j+8 where
 // (L >> 3) is odd, which makes every 16-lane group of a ds_read_b128 (8-lane group of a
@@ -1419,7 +1427,8 @@ constexpr int kBsChunkBytes = kMtN * 16;               // 9,984
 constexpr int kBsStateBytes = 8 * kBsChunkBytes;       // 79,872
 constexpr int kBsTabBytes = 256 * 4 + 256 * 8;         // 3,072
 constexpr uint32_t kBsFlagOff = kBsTabBytes + 2 * kBsStateBytes;  // u32 twisted-task count per half
-constexpr int kBsLdsBytes = (int)kBsFlagOff + 8;       // 162,824 <= 163,840
+constexpr uint32_t kBsProgOff = kBsFlagOff + 8;        // u32 per half-0 wave: its tasks < value are stored
+constexpr int kBsLdsBytes = (int)kBsProgOff + 4 * 6;   // 162,848 <= 163,840
 static_assert(kBsLdsBytes <= 163840, "slice kernel LDS");
 constexpr int kBsWaves = kBsHalfThreads / 64;          // waves per half (6)
 constexpr int kBsTaskWords = 128;                      // stream words per task
@@ -1467,10 +1476,16 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   const int half = __builtin_amdgcn_readfirstlane(tid >= kBsHalfThreads ? 1 : 0);
   const int ht = tid - half * kBsHalfThreads;
   const int hw = __builtin_amdgcn_readfirstlane(ht >> 6);
-  const int c = kBsChunksPerWg * (int)blockIdx.x + half;
-  const int nseeds = FULL ? kBsSeeds : a.nseeds;
-  const int64_t b0 = a.chunk_block[c], b1 = a.chunk_block[c + 1];
-  const int nwords = (int)(kMtN * (b1 - b0));  // < 2^31 (launch_apply_bs checks the chunk table's bound)
+  // slices (a pass of 33..64 seeds): both halves on plan chunks 2w, 2w+1, slice 0 with
+  // seeds [0, nA), slice 1 with [nA, nseeds) applied after slice 0's; split (<= 32 seeds):
+  // half h alone on plan chunk 2w+h with every seed
+  const bool split = a.split != 0;  // FULL: 32 seeds in each half either way
+  const int c = split ? 2 * (int)blockIdx.x + half : (int)blockIdx.x;  // index into the states
+  const int nA = FULL ? kBsSeeds : split ? a.nseeds : (a.nseeds + 1) / 2;
+  const int nseeds = FULL ? kBsSeeds : (half && !split ? a.nseeds - nA : nA);  // this half's seeds
+  const int sfirst = half && !split ? nA : 0;
+  const int64_t b0 = a.chunk_block[split ? c : 2 * c], b1 = a.chunk_block[split ? c + 1 : 2 * c + 2];
+  const int nwords = (int)(kMtN * (b1 - b0));  // < 2^31 (the host's plan keeps chunks shorter)
   const int ntask = (nwords + kBsTaskWords - 1) / kBsTaskWords;
   const uint32_t sbase = kBsTabBytes + (uint32_t)half * kBsStateBytes;
   const uint32_t flag = kBsFlagOff + 4u * (uint32_t)half;
@@ -1483,12 +1498,15 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   for (int i = ht; i < kMtN; i += kBsHalfThreads) {
     uint32_t w[32];
 #pragma unroll
-    for (int k = 0; k < 32; k++) w[k] = k < nseeds ? a.states[((size_t)k * a.nchunks + c) * kMtN + i] : 0u;
+    for (int k = 0; k < 32; k++)
+      w[k] = k < nseeds ? a.states[((size_t)(sfirst + k) * a.nchunks + c) * kMtN + i] : 0u;
     bs::transpose32(w);
     bs_store_row(sbase + 16u * (uint32_t)i, w);
   }
   if (ht == 0) lds32[flag / 4] = 0u;
+  if (half == 0 && ht < kBsWaves) lds32[kBsProgOff / 4 + ht] = 0u;
   __syncthreads();  // the only workgroup barrier
+  if (nseeds == 0) return;  // a one-seed pass: slice 1 is empty
 
   const int toff = 16 * (lane >> 3) + (lane & 7);  // the lane's words toff, toff + 8 of a task
   const bool flip = ((lane >> 3) & 1) != 0;
@@ -1496,7 +1514,7 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
 
   float gk[kBsSeeds];
 #pragma unroll
-  for (int k = 0; k < kBsSeeds; k++) gk[k] = a.g[k];
+  for (int k = 0; k < kBsSeeds; k++) gk[k] = a.g[half ? k + sfirst : k];
 
   // the lane's current segment (positions only grow)
   const int64_t wbase = (int64_t)kMtN * b0;  // stream position of the chunk's first word
@@ -1554,8 +1572,8 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   // bytes (row toff) and angle bytes (row toff + 8) as planes.  Streamed over the 8 chunk
   // arrays (planes 4q..4q+3): chunk q of every row of the task is loaded (V, M) before
   // any lane stores it -- through data dependence, since new plane 4q+3 needs V plane
-  // 4q+4 of chunk q+1, loaded one step ahead; U31 and V plane 0 are loaded first.  M rows
-  // lie 227 words back, outside the task, so the task never stores them.
+  // 4q+4 of chunk q+1, loaded one step ahead; U31 and V plane 0 are loaded first.  M
+  // rows lie 227 words back, outside the task, so the task never stores them.
   auto twist = [&](const int n, uint32_t (&oa)[8], uint32_t (&ob)[8]) {
     const int u1 = kBsTaskWords * n + toff;
     const bool valid = u1 < nwords;
@@ -1573,6 +1591,9 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
     rows(ib, av2, am2, au2);
     uint32_t M1[32], M2[32];  // the new rows
     const uint32_t U1 = lds_u32((int)au1), U2 = lds_u32((int)au2);
+    // (issuing all 34 loads of the task at once -- 164 VGPRs -- measured 5 % slower per
+    // pass: profiles/r03v_ab.log)
+    // (loads two or three chunk arrays ahead measured no faster: profiles/r03x_ab.log)
     u32x4_t va = lds_u4(av1), vb = lds_u4(av2), ma = lds_u4(am1), mb = lds_u4(am2);
     const uint32_t v0a = va.x, v0b = vb.x;
 #pragma unroll
@@ -1648,6 +1669,22 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
     ST::store_pair(sl.addr, out);
   };
 
+  const bool ordered = !split;  // half 1 depends on half 0's stores
+  // ---- half 0 publishes its task m's parameters as stored (the wave's global stores
+  // done: vmcnt(0), the workgroup-scope release); half 1 waits for that before loading them
+  const uint32_t prog = kBsProgOff + 4u * (uint32_t)hw;
+  auto publish_stored = [&](const int m) {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    if (lane == 0) *(volatile lds_u32_t*)(size_t)prog = (uint32_t)m + 1u;
+  };
+  auto await_stored = [&](const int m) {
+    if (m >= ntask) return;
+    const uint32_t pm = kBsProgOff + 4u * (uint32_t)(m % kBsWaves);
+    while (__builtin_amdgcn_readfirstlane(bs_flag_load(pm)) < (uint32_t)m + 1u) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+  };
+
   // ---- task n: wait for task n-1's twist, twist, publish, chain; fetches task n + 6
   // into nx (past the last task: the sink)
   auto task = [&](const int n, const Slot& sl, Slot& nx) {
@@ -1658,6 +1695,11 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
     twist(n, oa, ob);
     if (lane == 0) bs_flag_store(flag, (uint32_t)n + 1u);
     __builtin_amdgcn_s_setprio(0);
+    if (ordered && half == 0) {
+      if (n >= kBsWaves) publish_stored(n - kBsWaves);  // the store of the wave's previous task
+    } else if (ordered) {
+      await_stored(n + kBsWaves);
+    }
     nx = fetch(n + kBsWaves);
     chain(sl, oa, ob);
   };
@@ -1665,13 +1707,18 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   // two named slots and a loop unrolled by two: a slot copy on the back edge would wait
   // for the load -- and the store before it -- at the top of every task
   if (hw >= ntask) return;
+  if (ordered && half) await_stored(hw);
   Slot s0 = fetch(hw), s1;
-  for (int n = hw;;) {
+  int n = hw;
+  for (;;) {
     task(n, s0, s1);
-    if ((n += kBsWaves) >= ntask) break;
+    if (n + kBsWaves >= ntask) break;
+    n += kBsWaves;
     task(n, s1, s0);
-    if ((n += kBsWaves) >= ntask) break;
+    if (n + kBsWaves >= ntask) break;
+    n += kBsWaves;
   }
+  if (ordered && half == 0) publish_stored(n);  // the wave's last task
 }
 
 // ------------------------------------------------------------------ irregular kernel
@@ -2154,18 +2201,21 @@ template <int MODE, bool FULL>
 static int launch_apply_bs_m(const ApplyBsArgs& a, void* stream) {
   static PerDevice attr;
   if (int e = ensure_lds_attr(attr, &fks_apply_bs_kernel<MODE, FULL>, kBsLdsBytes)) return e;
-  hipLaunchKernelGGL((fks_apply_bs_kernel<MODE, FULL>), dim3((unsigned)(a.nchunks / kBsChunksPerWg)),
+  hipLaunchKernelGGL((fks_apply_bs_kernel<MODE, FULL>), dim3((unsigned)(a.split ? a.nchunks / 2 : a.nchunks)),
                      dim3(kBsThreads), kBsLdsBytes, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 
 template <int MODE>
 static int launch_apply_bs_t(const ApplyBsArgs& a, void* stream) {
-  return a.nseeds == kBsSeeds ? launch_apply_bs_m<MODE, true>(a, stream) : launch_apply_bs_m<MODE, false>(a, stream);
+  // FULL: 32 seeds in each half (a split pass of 32, a two-slice pass of 64)
+  const bool full = a.nseeds == (a.split ? kBsSeeds : kBsPassSeeds);
+  return full ? launch_apply_bs_m<MODE, true>(a, stream) : launch_apply_bs_m<MODE, false>(a, stream);
 }
 
 int launch_apply_bs(const ApplyBsArgs& a, void* stream) {
-  if (a.nseeds < 1 || a.nseeds > kBsSeeds || a.nchunks < kBsChunksPerWg || a.nchunks % kBsChunksPerWg)
+  if (a.nseeds < 1 || a.nseeds > (a.split ? kBsSeeds : kBsPassSeeds) || a.nchunks < 1 ||
+      (a.split && a.nchunks % 2))
     return -FKS_EINVAL;
   int e = ensure_tables();
   if (e) return e;

@@ -150,29 +150,34 @@ struct IrrArgs {
   int32_t mode;
 };
 
-// bf16 slice kernel (fks_apply_bs_kernel): 32 seeds per pass, bit-sliced generator
-// state; one workgroup per CU holds two chunks (two 384-thread halves of six waves, each
-// wave twisting and updating 128-word tasks of its chunk) and LDS = 3 KB of tables +
-// 2 x 79,872 B of state + two task flags.
-constexpr int kBsSeeds = 32;
+// bf16 slice kernel (fks_apply_bs_kernel): up to 64 seeds per pass; one workgroup per CU
+// with two bit-sliced 32-seed states (one plane word per 32 seeds) in two 384-thread
+// halves of six waves, each wave twisting and updating 128-word tasks; LDS = 3 KB of
+// tables + 2 x 79,872 B of state + task flags.  The plan cuts the stream into 2 x (one per
+// CU) chunks; a pass of 33..64 seeds runs two SLICES on one chunk PAIR (half 1 applies
+// seeds [ceil(n/2), n) after half 0 applied [0, ceil(n/2))), a pass of <= 32 seeds runs
+// one slice on each chunk of the pair (split).
+constexpr int kBsSeeds = 32;                  // seeds per slice (bits of a plane word)
+constexpr int kBsPassSeeds = 2 * kBsSeeds;    // seeds per launch
 constexpr int kBsHalfThreads = 384;
 constexpr int kBsThreads = 2 * kBsHalfThreads;
-constexpr int kBsChunksPerWg = 2;
+constexpr int kBsChunksPerWg = 2;  // plan chunks per workgroup
 // reconstructs of more seeds than one 19-seed pass take the slice kernel for their
 // bf16 fast segments
 constexpr int kBsMinSeeds = kMaxSeedsPerPass + 1;
-constexpr int kJumpMaxSeeds = kBsSeeds > kMaxSeedsPerPass ? kBsSeeds : kMaxSeedsPerPass;
+constexpr int kJumpMaxSeeds = kBsPassSeeds > kMaxSeedsPerPass ? kBsPassSeeds : kMaxSeedsPerPass;
 
 struct ApplyBsArgs {
   const uint32_t* states;       // [nseeds][nchunks][624] generator windows at chunk starts
-  float g[kBsSeeds];            // update multiplier per seed / delta coefficient
+  float g[kBsPassSeeds];        // update multiplier per seed / delta coefficient
   const DevSeg* segs;           // bf16 fast segments, sorted by start
-  const int64_t* chunk_block;   // [nchunks + 1], nchunks = kBsChunksPerWg x workgroups
+  const int64_t* chunk_block;   // [2 x workgroups + 1] plan chunks
   uint64_t* sink;               // workspace sink for idle lanes' loads/stores
   int32_t nsegs;
-  int32_t nchunks;
-  int32_t nseeds;               // 1..32
+  int32_t nchunks;              // chunks of the states array: workgroups (slices) or 2 x workgroups (split)
+  int32_t nseeds;               // slices: 1..64, slice 0 takes seeds [0, ceil(n/2)), slice 1 the rest; split: 1..32
   int32_t mode;
+  int32_t split;                // 1: one slice per plan chunk; 0: two slices on a chunk pair
 };
 
 struct JumpArgs {
@@ -182,6 +187,7 @@ struct JumpArgs {
   uint32_t* states;             // [nseeds][nchunks][624]
   int32_t nchunks;
   int32_t chunks_per_wg;
+  int32_t stride;               // chunk c starts at chunk_block[c * stride] (polys likewise); 0 = 1
 };
 
 // ---- torch_rocm stream (FKS_STREAM_ROCM): torch.normal on a HIP device ----

@@ -1,12 +1,15 @@
-"""GPU parity of the bf16 slice kernel (fks_apply_bs_kernel: bit-sliced MT19937, 32 seeds
-per pass), which takes the bf16 fast segments of every reconstruct of K >= 20 seeds.
+"""GPU parity of the bf16 slice kernel (fks_apply_bs_kernel: bit-sliced MT19937, 64 seeds
+per pass as two 32-seed slices, the second applied after the first), which takes the bf16
+fast segments of every reconstruct of K >= 20 seeds.
 
 Bar: bit-exact against the CPU oracle (itself pinned to the reference's golden vectors).
-Cases: a full slice (K = 32), a full slice plus one seed, the smallest slice call
-(K = 20), three slices with a partial one (K = 95); the three update modes (weight decay
-on every tensor, on none, mixed); many small segments switching inside MT blocks; fp32
-tensors interleaved (they stay on the 19-seed kernel); a one-block stream (one of the
-workgroup's two chunks empty); element shards.
+Cases: the smallest slice call (K = 20: slices of 10 + 10), one full slice (K = 32:
+16 + 16), 33 (17 + 16), a full pass (K = 64), a full pass plus a one-seed pass (K = 65:
+the second slice of the last pass is empty), 95 (64 + 16 + 15), 127 (64 + 32 + 31); the
+three update modes (weight decay on every tensor, on none, mixed); many small segments
+switching inside MT blocks; fp32 tensors interleaved (they stay on the 19-seed kernel); a
+one-block stream (one task per chunk, five of a half's six waves idle); element shards;
+chunks of many MT blocks.
 """
 import numpy as np
 import pytest
@@ -29,7 +32,7 @@ def _seeds(k, seed):
 SHAPES = [2**17, 48, 1234 * 16, 2**16, 4096 * 3, 16, 624 * 16 + 32]
 
 
-@pytest.mark.parametrize("k", [20, 32, 33, 95])
+@pytest.mark.parametrize("k", [20, 32, 33, 64, 65, 95, 127])
 @pytest.mark.parametrize("wdmode", ["all", "none", "mixed"])
 def test_slice_reconstruct_vs_oracle(k, wdmode):
     arrays = rand_params(SHAPES, "bfloat16", seed=k)
@@ -64,7 +67,7 @@ def test_slice_many_small_segments_and_fp32_interleaved():
 
 
 def test_slice_one_block_stream():
-    """A 16-element stream: one MT block, so one of the workgroup's chunks is empty."""
+    """A 16-element stream: one MT block, one chunk of one task."""
     arrays = rand_params([16], "bfloat16", seed=2)
     seeds, vals = _seeds(40, seed=3)
     got = _gpu_reconstruct(arrays, "bfloat16", [1e-3], [0.01], seeds, vals)
@@ -92,19 +95,19 @@ def test_slice_element_shards_equal_oracle(nshards):
 @pytest.mark.parametrize("k", [32, 95])
 @pytest.mark.parametrize("wd", [0.0, None])
 def test_slice_multiblock_chunks_vs_oracle(k, wd):
-    """The regime of every 7B launch: each of the slice kernel's 512 chunks spans many MT
-    blocks, so the twist wave carries block b into b + 1 inside a chunk (the bench's
-    chain: weight decay 0.0 -> kModeUpdateWd0, None -> kModeUpdateNoWd, both with the
-    packed (C,S) table).  4.2 M bf16 params = 6,771 MT blocks (13 per chunk); K = 32 is
-    one full pass, K = 95 three passes with a partial one.  Bit-exact against the oracle
-    (fedkseed.py:136-141, zo_utils.py:47-52)."""
+    """The regime of every 7B launch: each of the slice kernel's 256 chunks spans many MT
+    blocks, so the tasks' twists carry block b into b + 1 inside a chunk and the second
+    slice waits on the first one's stores (the bench's chain: weight decay 0.0 ->
+    kModeUpdateWd0, None -> kModeUpdateNoWd).  4.2 M bf16 params = 6,771 MT blocks (26
+    per chunk, 127 tasks); K = 32 is one pass of two 16-seed slices, K = 95 a full pass
+    and a partial one.  Bit-exact against the oracle (fedkseed.py:136-141, zo_utils.py:47-52)."""
     from fate_llm.algo.fedkseed import codec
     dev = _dev()
     shapes = [1 << 22, 624 * 48 + 32]
     arrays = rand_params(shapes, "bfloat16", seed=1000 + k)
     seeds, vals = _seeds(k, seed=2000 + k)
     ts = [from_np(a, "bfloat16", dev) for a in arrays]
-    assert codec.stream_length(ts) // 624 >= 8 * 512, "fewer than 8 MT blocks per chunk"
+    assert codec.stream_length(ts) // 624 >= 16 * 256, "fewer than 16 MT blocks per chunk"
     specs = [codec.ParamSpec(t, lr=1e-5, weight_decay=wd) for t in ts]
     codec.directional_step(specs, seeds, vals)
     torch.cuda.synchronize()

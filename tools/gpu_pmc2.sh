@@ -35,4 +35,4 @@ if [ -n "$UBENCH" ]; then
   done
 fi
 python3 tools/pmc2_show.py ${VARIANTS:-full}
-for v in ${VARIANTS:-full}; do python3 tools/summarize_pmc2.py "${TAG:-r02}_$v" $v $((1 << 28)) 32 > /dev/null; done
+for v in ${VARIANTS:-full}; do python3 tools/summarize_pmc2.py "${TAG:-r02}_$v" $v $((1 << 28)) ${PMC_SEEDS:-64} > /dev/null; done

@@ -17,7 +17,7 @@ done
 libs=("")
 for v in "$@"; do libs+=("fate-llm_amd/build/libfks_$v.so"); done
 for wd in ${AB_WD:-0.0}; do
-  AB_WD=$wd AB_N=$((1 << 28)) AB_K=${AB_K:-128} AB_SEEDS=32 timeout -k 10 400 python3 -u tools/ab_apply.py "${libs[@]}" \
+  AB_WD=$wd AB_N=$((1 << 28)) AB_K=${AB_K:-128} AB_SEEDS=${AB_SEEDS:-64} timeout -k 10 400 python3 -u tools/ab_apply.py "${libs[@]}" \
     >> gpurun_out/${tag}_ab.log 2>&1 || { cat gpurun_out/${tag}_ab.log; exit 99; }
 done
 cat gpurun_out/${tag}_ab.log
