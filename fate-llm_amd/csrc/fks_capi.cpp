@@ -697,6 +697,7 @@ struct PhxPlan {
   int device = 0;
   int nt = 0;           // table entries (tensors with work items)
   int64_t items = 0;    // work items of all tensors
+  int wd_mode = kModeUpdate;  // kModeUpdateWd / NoWd / Wd0 when every tensor shares the form
 };
 std::vector<PhxPlan*> g_phx;
 
@@ -867,6 +868,16 @@ PhxPlan* get_phx_plan(const fks_tensor* t, int nt, const double* scales) {
   P->last_use = ++g_cache_clock;
   P->nt = (int)tab.size();
   P->items = items;
+  {  // the launch-wide weight-decay form of a reconstruct (as CachedPlan::wd_mode)
+    size_t nwd = 0, nwd0 = 0;
+    for (const PhxTensor& x : tab) {
+      nwd += (x.flags & FKS_HAS_WD) ? 1 : 0;
+      nwd0 += ((x.flags & FKS_HAS_WD) && x.wd == 0.0f) ? 1 : 0;  // +0.0 or -0.0
+    }
+    if (!tab.empty() && nwd0 == tab.size()) P->wd_mode = kModeUpdateWd0;
+    else if (!tab.empty() && nwd == tab.size()) P->wd_mode = kModeUpdateWd;
+    else if (!tab.empty() && nwd == 0) P->wd_mode = kModeUpdateNoWd;
+  }
   (void)hipGetDevice(&P->device);
   const size_t bytes = std::max<size_t>(sizeof(PhxTensor) * tab.size(), 256);
   if (hipMalloc(&P->dev, bytes) != hipSuccess) {
@@ -901,7 +912,7 @@ void run_philox(const fks_tensor* t, int nt, const uint64_t* seeds, const double
   a.t = static_cast<const PhxTensor*>(P->dev);
   a.nt = P->nt;
   a.gdev = gdev;
-  a.mode = mode;
+  a.mode = mode == kModeUpdate ? P->wd_mode : mode;
   a.item_lo = (int64_t)((__int128)P->items * shard / nshards);
   a.item_hi = (int64_t)((__int128)P->items * (shard + 1) / nshards);
   if (a.item_lo >= a.item_hi) return;

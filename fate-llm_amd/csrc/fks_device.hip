@@ -1933,13 +1933,25 @@ __global__ __launch_bounds__(kApplyThreads) void fks_irregular_kernel(IrrArgs a)
 // CPU stream.  One thread per work item (tensor, idx, j): for every seed in order one
 // Philox4x32-10 call at counter (off4 + j, idx, 0) and key (seed), two rocrand Box-Muller
 // pairs, four elements idx + stride (4 j + i).  Counter-mode: no generator state, no jump.
-__device__ __forceinline__ uint4 philox4x32_10(uint64_t ctr, uint32_t idx, uint64_t seed) {
+// Round 1 of Philox4x32-10 multiplies the COUNTER only (the key enters by xor), so an
+// item computes it once for all the seeds of a pass.
+struct PhxRound1 {
+  uint32_t a0, a2;  // hi(M1 c2) ^ c1, hi(M0 c0) ^ c3: xored with the key halves
+  uint32_t c1, c3;  // lo(M1 c2), lo(M0 c0)
+};
+__device__ __forceinline__ PhxRound1 philox_round1(uint64_t ctr, uint32_t idx) {
+  const uint64_t m0 = (uint64_t)0xD2511F53u * (uint32_t)ctr, m1 = (uint64_t)0xCD9E8D57u * idx;
+  return PhxRound1{(uint32_t)(m1 >> 32) ^ (uint32_t)(ctr >> 32), (uint32_t)(m0 >> 32), (uint32_t)m1, (uint32_t)m0};
+}
+__device__ __forceinline__ uint4 philox4x32_10(const PhxRound1& r1, uint64_t seed) {
   // Random123 Philox4x32-10 as rocrand_philox4x32_10.h:270-303 (counter (x, y, z, w) =
   // (ctr lo, ctr hi, subsequence lo, hi), key (seed lo, hi), bumped by the Weyl constants)
-  uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32), c2 = idx, c3 = 0u;
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  uint32_t c0 = r1.a0 ^ k0, c1 = r1.c1, c2 = r1.a2 ^ k1, c3 = r1.c3;
+  k0 += 0x9E3779B9u;
+  k1 += 0xBB67AE85u;
 #pragma unroll
-  for (int r = 0; r < 10; r++) {
+  for (int r = 1; r < 10; r++) {
     const uint64_t m0 = (uint64_t)0xD2511F53u * c0, m1 = (uint64_t)0xCD9E8D57u * c2;
     const uint32_t n0 = (uint32_t)(m1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(m0 >> 32) ^ c3 ^ k1;
     c1 = (uint32_t)m1;
@@ -1969,6 +1981,9 @@ __device__ __forceinline__ float phx_cast(float v) {  // static_cast<scalar_t>(f
   return DT == FKS_F32 ? v : Traits<DT>::rnd(v);
 }
 
+// The item's four elements through every seed of the pass, in seed order, as two packed
+// pairs (apply_pair: the values of apply_one); MODE may be a launch-wide weight-decay
+// specialisation of kModeUpdate (kModeUpdateWd / NoWd / Wd0, as the CPU stream's kernels).
 template <int DT, int MODE>
 __device__ __forceinline__ void phx_item(const PhiloxArgs& a, const PhxTensor& T, int64_t r) {
   using TR = Traits<DT>;
@@ -1988,15 +2003,23 @@ __device__ __forceinline__ void phx_item(const PhiloxArgs& a, const PhxTensor& T
   const bool dv = MODE == kModePerturbUpdate && a.gdev;
   const bool upd = dv ? dev_value_apply(a.gdev) : true;
   const float gd = dv ? dev_value_g<DT>(a.gdev) : 0.0f;
+  const PhxRound1 r1 = philox_round1(T.off4 + j, idx);
+  f32x2_t pA = {p[0], p[1]}, pB = {p[2], p[3]};
   for (int k = 0; k < a.nseeds; k++) {
     const uint64_t seed = a.seeds[k];  // wave-uniform: scalar loads
     const float g = dv ? gd : a.g[3 * k + DT];
-    const uint4 w = philox4x32_10(T.off4 + j, idx, seed);
-    const float2 r1 = rocrand_box_muller(w.x, w.y), r2 = rocrand_box_muller(w.z, w.w);
-    const float rv[4] = {r1.x, r1.y, r2.x, r2.y};
-#pragma unroll
-    for (int i = 0; i < 4; i++) p[i] = apply_one<DT>(p[i], phx_cast<DT>(rv[i]), g, T.lr, T.wd, has_wd, MODE, T.ps, upd);
+    const uint4 w = philox4x32_10(r1, seed);
+    const float2 b1 = rocrand_box_muller(w.x, w.y), b2 = rocrand_box_muller(w.z, w.w);
+    const f32x2_t zA = {phx_cast<DT>(b1.x), phx_cast<DT>(b1.y)}, zB = {phx_cast<DT>(b2.x), phx_cast<DT>(b2.y)};
+    if (MODE == kModeWriteZ) {
+      pA = zA;
+      pB = zB;
+    } else {
+      pA = apply_pair<DT, MODE>(pA, zA, g, T.lr, T.wd, has_wd, T.ps, upd);
+      pB = apply_pair<DT, MODE>(pB, zB, g, T.lr, T.wd, has_wd, T.ps, upd);
+    }
   }
+  p[0] = pA.x; p[1] = pA.y; p[2] = pB.x; p[3] = pB.y;
 #pragma unroll
   for (int i = 0; i < 4; i++)
     if (on[i]) TR::store(T.ptr, e[i], p[i]);
@@ -2005,12 +2028,14 @@ __device__ __forceinline__ void phx_item(const PhiloxArgs& a, const PhxTensor& T
 template <int MODE>
 __global__ __launch_bounds__(256) void fks_philox_kernel(PhiloxArgs a) {
   const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  int t0 = 0;  // items only grow: the search starts at the previous item's tensor
   for (int64_t it = a.item_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; it < a.item_hi; it += step) {
-    int lo = 0, hi = a.nt - 1;  // the last tensor whose first item is <= it
+    int lo = t0, hi = a.nt - 1;  // the last tensor whose first item is <= it
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
       if (a.t[mid].item0 <= it) lo = mid; else hi = mid - 1;
     }
+    t0 = lo;
     const PhxTensor T = a.t[lo];
     switch (T.dtype) {
       case FKS_F32: phx_item<FKS_F32, MODE>(a, T, it - T.item0); break;
@@ -2291,6 +2316,9 @@ int launch_philox(const PhiloxArgs& a, void* stream) {
   if (a.nseeds < 1 || a.nt < 1) return -FKS_EINVAL;
   switch (a.mode) {
     case kModeUpdate: return launch_philox_m<kModeUpdate>(a, stream);
+    case kModeUpdateWd: return launch_philox_m<kModeUpdateWd>(a, stream);
+    case kModeUpdateNoWd: return launch_philox_m<kModeUpdateNoWd>(a, stream);
+    case kModeUpdateWd0: return launch_philox_m<kModeUpdateWd0>(a, stream);
     case kModePerturb: return launch_philox_m<kModePerturb>(a, stream);
     case kModePerturbUpdate: return launch_philox_m<kModePerturbUpdate>(a, stream);
     case kModeWriteZ: return launch_philox_m<kModeWriteZ>(a, stream);
