@@ -463,7 +463,6 @@ struct CachedPlan {
   int wd_mode[3] = {kModeUpdate, kModeUpdate, kModeUpdate};  // kModeUpdateWd / NoWd when uniform
   bool have_reg = false, have_irr = false;
   bool have_bs = false;  // bf16 fast segments with their slice-kernel plan (non-small calls)
-  int64_t bs_blocks = 0; // MT blocks the slice-kernel plan covers
   uint64_t chunk_hash = 0;  // the chunk starts (regular + irregular): what a seed's windows depend on
   int64_t reg_lo = 0, reg_hi = 0;  // MT blocks [reg_lo, reg_hi) the regular chunks cover
   uint64_t bf16_hash = 0;  // the bf16 segments' stream ranges: which blocks a z-index store covers
@@ -569,7 +568,6 @@ CachedPlan* build_plan(const fks_tensor* t, int nt, const double* scales, uint64
   C->have_bs = !small && !L.segs[FKS_BF16].empty();
   if (C->have_bs) {
     BP = make_plan_n(br, bs_nchunks(br.hi - br.lo));
-    C->bs_blocks = br.hi - br.lo;
     // the slice kernel indexes a chunk's stream words in 32 bits (< 2^31: 3.4 M blocks
     // per plan chunk pair, a 5.6e11-parameter stream at 512 chunks); longer chunks take the 19-seed kernel
     for (int c = 0; C->have_bs && c < BP.nchunks; c++)
@@ -1021,14 +1019,14 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
     return value_kind == FKS_VALUE_TENSOR ? round_to_dtype(values[s], d) : (float)values[s];
   };
   if (use_bs) {
-    // Passes of 64 seeds as two slices per chunk pair (one jump per seed and chunk PAIR)
-    // or of 32 seeds, one slice per plan chunk (a serial twist chain half as long per
-    // chunk).  Per seed: two slices 0.395 ps per parameter + 36 us of jumps, one slice
-    // 0.387 ps + 71 us (profiles/r03w_ab.log, r03b/r03c bench lines): two slices pay
-    // below 4e9 parameters (every element shard of a multi-GPU 7B, the smaller models),
-    // one slice above (a whole 7B buffer).  FKS_BS_SLICES=1|2 forces one (diagnostics).
-    int slices = (C->Z.bs_chunks > 0 && (double)(kMtN * (double)C->bs_blocks) < 4e9) ? 2 : 1;
-    if (const char* e = std::getenv("FKS_BS_SLICES")) slices = (e[0] == '1') ? 1 : (e[0] == '2') ? 2 : slices;
+    // Passes of 64 seeds as two slices per chunk pair (one jump per seed and chunk PAIR),
+    // the remainder of <= 32 seeds one slice per plan chunk.  The apply costs the same per
+    // seed either way (6.785 ms per 64 seeds against 2 x 3.388 ms over 2^28 parameters,
+    // profiles/r03y_*ab.log) and half the jumps go: the 7B bench 10.92 s against 11.03 s
+    // for 32-seed passes on one box (profiles/r03g_*.log).  FKS_BS_SLICES=1 forces 32-seed
+    // passes (diagnostics, A/B).
+    int slices = 2;
+    if (const char* e = std::getenv("FKS_BS_SLICES")) slices = (e[0] == '1') ? 1 : 2;
     const int per_pass = slices == 2 ? kBsPassSeeds : kBsSeeds;
     for (int s0 = 0; s0 < k; s0 += per_pass) {
       const int nb = std::min(per_pass, k - s0);
