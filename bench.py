@@ -14,15 +14,22 @@ anything touches the GPU, and exits with its status; run under torch.distributed
 directly, WORLD_SIZE must equal --gpus.
 
 --mode sequential (default, bit-exact):
-  --scaling weak (default): every rank reconstructs its own 7B buffer from the same
-    K=4096 list -- the FedKSeed deployment, where each client GPU rebuilds its model from
-    the (seed, sum) list the arbiter broadcasts (fedkseed.py:128-141); no collective;
-    value = N buffers / the slowest rank's time;
-  --scaling strong: one 7B buffer cut into N equal runs of MT19937 blocks, rank r
+  --scaling strong (default): BASELINE's 8xMI355X config -- one 7B buffer, K=4096,
+    split over the GPUs: the buffer is cut into N equal runs of MT19937 blocks and rank r
     reconstructs run r (element sharding: every element still sees every seed in order,
     so the union is bit-identical to N = 1 and no collective touches the data path);
-    --gather adds the all-gather that leaves the whole buffer on every rank (N RCCL
-    broadcasts of the shards), timed separately.
+    value = ONE buffer / the slowest rank's time; --gather adds the all-gather that
+    leaves the whole buffer on every rank (N RCCL broadcasts of the shards), timed
+    separately;
+  --scaling weak (opt-in, reported under its own metric name): every rank reconstructs
+    its own 7B buffer from the same K=4096 list -- the FedKSeed deployment, where each
+    client GPU rebuilds its model from the (seed, sum) list the arbiter broadcasts
+    (fedkseed.py:128-141); no collective; value = N buffers / the slowest rank's time.
+
+Under torch.distributed.run (WORLD_SIZE in the environment) the ranks always form a
+process group -- RCCL ("nccl") unless FKS_BENCH_SHARE_GPU=1 -- even at WORLD_SIZE=1, so
+the timing's max-over-ranks, --gather and the seed-shard all-reduce run through the
+collective library on a one-GPU box too (tests/test_gpu_rccl.py).
 
 --mode seed-shard: the north star's C3 variant.  Rank r takes a contiguous 1/N of the
 seeds, accumulates its f32 delta over the whole buffer (fks_delta_accumulate), one RCCL
@@ -257,7 +264,7 @@ def timed_steps(step, args, world, sync):
 
 
 def max_over_ranks(dt, world, device):
-    if world == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return dt
     t = torch.tensor([dt], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -295,7 +302,8 @@ def run(args, world, rank, local):
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    distributed = "WORLD_SIZE" in os.environ  # launched by torch.distributed.run (any world size)
+    if distributed:
         if share:
             dist.init_process_group("gloo")
         else:
@@ -337,7 +345,7 @@ def run(args, world, rank, local):
         dt = timed_steps(step, args, world, sync)
     dt = max_over_ranks(dt, world, dev)
     gather_ms = None
-    if args.gather and world > 1 and not seed_shard and not weak:
+    if args.gather and distributed and not seed_shard and not weak:
         # every rank ends with the whole buffer: one broadcast of each element shard (the
         # bench's buffer is one flat tensor and all its tensors are fast segments, so a
         # shard's stream words are its element range)
@@ -411,21 +419,28 @@ def run(args, world, rank, local):
                              "wave-instruction (profiles/r02_ubench_issue3.log)")}
     # the north star's roof: algorithmic HBM bytes of the WHOLE reconstruct (read + write the
     # buffer once, SURVEY.md §8(d): 2 N elt) over the reconstruct time; the per-pass figure
-    # (each 64-seed launch streams its shard once) is reported beside it, named as such
+    # (each 64-seed launch streams its shard once) is reported beside it, named as such.
+    # Per GPU, against one GPU's peak: a strong element shard reads + writes its own run
+    # once; a weak rank its whole buffer; a seed-shard rank accumulates (and applies) over
+    # the whole buffer too
     elt = 4 if seed_shard else 2
     alg_bytes_step = 2 * total * 2 * (world if weak else 1)
-    hbm_ach = alg_bytes_step / (dt / args.steps) / 1e9 / world  # per GPU, against one GPU's peak
+    rank_alg_bytes = 2 * rank_params * 2
+    hbm_ach = rank_alg_bytes / (dt / args.steps) / 1e9
     traffic = pmc.get("hbm_bytes_per_param_per_launch")
     hbm = {"bound": "hbm", "achieved": round(hbm_ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(hbm_ach / HBM_PEAK_GBS, 7),
            "traffic": (round(traffic * rank_params) if traffic and not seed_shard and not withheld else None),
-           "alg_bytes_per_step": alg_bytes_step,
+           "alg_bytes_per_step": alg_bytes_step, "alg_bytes_per_step_this_gpu": rank_alg_bytes,
            "per_pass": {"alg_bytes_per_launch": 2 * rank_params * elt,
                         "achieved_GBps": round(2 * rank_params * elt / avg_apply_s / 1e9, 2),
                         "note": f"one launch reads + writes its shard once ({round(seeds_per_launch)} seeds); a reconstruct is "
                                 f"{round(n_apply / n_steps_prof)} such passes"}}
+    metric = "GB/s param buffer reconstructed from (seed,scalar) list, device-resident"
+    if weak and world > 1:
+        metric += " [weak scaling: one buffer per GPU]"
     out = {
-        "metric": "GB/s param buffer reconstructed from (seed,scalar) list, device-resident",
+        "metric": metric,
         "value": round(value, 4), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 2), "higher_is_better": True, "scaling": "weak" if weak else "strong",
         "mode": args.mode, "vs_baseline": None, "dtype": "bf16",
@@ -445,7 +460,7 @@ def run(args, world, rank, local):
         "build_id": build_id,
         "jump_kernel_ms_per_step": round(prof.jump_ms / n_steps_prof, 2),
     }
-    if world > 1:
+    if distributed:
         out["backend"] = dist.get_backend()
         if share:
             out["shared_gpu"] = True  # a rehearsal, not a measurement
@@ -459,7 +474,7 @@ def run(args, world, rank, local):
         out["cpu_baseline"] = cpu_baseline(args.cpu_budget, wd)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
     return 0
 
@@ -479,9 +494,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=24.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("sequential", "seed-shard"), default="sequential")
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
-                    help="sequential mode, N > 1: weak = a 7B buffer per GPU (default), strong = one buffer "
-                         "element-sharded over the GPUs")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
+                    help="sequential mode, N > 1: strong = one buffer element-sharded over the GPUs (default, "
+                         "BASELINE's 8xMI355X config); weak = a 7B buffer per GPU (opt-in, own metric name)")
     ap.add_argument("--gather", action="store_true", help="N > 1, strong: all-gather the shards afterwards")
     ap.add_argument("--selftest", action="store_true", help="CPU/gloo check of the launcher and timing logic")
     args = ap.parse_args()

@@ -696,6 +696,9 @@ struct PhxPlan {
   int nt = 0;           // table entries (tensors with work items)
   int64_t items = 0;    // work items of all tensors
   int wd_mode = kModeUpdate;  // kModeUpdateWd / NoWd / Wd0 when every tensor shares the form
+  std::vector<PhxTensor> tab;  // host copy of the table
+  std::vector<int64_t> elem0;  // per entry: its first element in the concatenation of ALL the call's tensors
+  int64_t elems = 0;           // elements of all the call's tensors
 };
 std::vector<PhxPlan*> g_phx;
 
@@ -832,10 +835,12 @@ PhxPlan* get_phx_plan(const fks_tensor* t, int nt, const double* scales) {
     }
   const int64_t max_grid = (int64_t)device_cu_count() * (device_max_threads_per_cu() / 256);
   std::vector<PhxTensor> tab;
+  std::vector<int64_t> elem0;
   uint64_t off4 = 0;
-  int64_t items = 0;
+  int64_t items = 0, elems = 0;
   for (int i = 0; i < nt; i++) {
     const int64_t n = t[i].numel;
+    elems += n;
     if (n == 0) continue;  // torch draws nothing for an empty tensor (the offset stays)
     if (n * (int64_t)elem_size(t[i].dtype) > (int64_t)INT32_MAX)
       throw Error(-FKS_ENOTSUP, "tensor " + std::to_string(i) +
@@ -856,6 +861,7 @@ PhxPlan* get_phx_plan(const fks_tensor* t, int nt, const double* scales) {
       x.flags = t[i].flags & FKS_HAS_WD;
       x.ps = scales ? (float)scales[i] : 0.0f;
       tab.push_back(x);
+      elem0.push_back(elems - n);
       items += stride * J;
     }
     off4 += (uint64_t)J;
@@ -866,6 +872,7 @@ PhxPlan* get_phx_plan(const fks_tensor* t, int nt, const double* scales) {
   P->last_use = ++g_cache_clock;
   P->nt = (int)tab.size();
   P->items = items;
+  P->elems = elems;
   {  // the launch-wide weight-decay form of a reconstruct (as CachedPlan::wd_mode)
     size_t nwd = 0, nwd0 = 0;
     for (const PhxTensor& x : tab) {
@@ -887,6 +894,8 @@ PhxPlan* get_phx_plan(const fks_tensor* t, int nt, const double* scales) {
     delete P;
     throw Error(-FKS_EHIP, "torch_rocm plan upload");
   }
+  P->tab = std::move(tab);
+  P->elem0 = std::move(elem0);
   if (g_phx.size() >= kPlanCacheEntries) {
     auto victim = std::min_element(g_phx.begin(), g_phx.end(),
                                    [](const PhxPlan* a, const PhxPlan* b) { return a->last_use < b->last_use; });
@@ -895,6 +904,35 @@ PhxPlan* get_phx_plan(const fks_tensor* t, int nt, const double* scales) {
   }
   g_phx.push_back(P);
   return P;
+}
+
+// Element shards of the torch_rocm stream.  Work item r of a tensor is (idx, j) =
+// (r % S, r / S) and covers elements idx + S (4 j + i), i < 4: a ROW of S items (one j)
+// covers the 4 S consecutive elements [4 j S, 4 (j + 1) S).  Shard boundaries are the
+// equal item splits rounded to the nearest row start, so every shard updates whole rows:
+// one contiguous run of elements of the call's tensors laid end to end (fks_shard_census).
+int phx_entry(const PhxPlan* P, int64_t b) {  // the last entry whose first item is <= b
+  int lo = 0, hi = P->nt - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (P->tab[mid].item0 <= b) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+int64_t phx_boundary(const PhxPlan* P, int shard, int nshards) {
+  const int64_t b = (int64_t)((__int128)P->items * shard / nshards);
+  if (b <= 0 || b >= P->items) return std::max<int64_t>(0, std::min(b, P->items));
+  const PhxTensor& T = P->tab[phx_entry(P, b)];
+  const int64_t S = T.stride, rows = (T.numel - 1) / (4 * S) + 1;
+  const int64_t j = std::min(rows, (b - T.item0 + S / 2) / S);
+  return T.item0 + j * S;
+}
+// the first element (in the concatenation of all the call's tensors) of item boundary b
+int64_t phx_boundary_elem(const PhxPlan* P, int64_t b) {
+  if (b >= P->items) return P->elems;
+  const int k = phx_entry(P, b);
+  const PhxTensor& T = P->tab[k];
+  return P->elem0[k] + std::min<int64_t>(T.numel, 4 * ((b - T.item0) / T.stride) * (int64_t)T.stride);
 }
 
 // the torch_rocm stream: seeds in passes of kPhxSeeds (by value in the kernel arguments);
@@ -911,8 +949,8 @@ void run_philox(const fks_tensor* t, int nt, const uint64_t* seeds, const double
   a.nt = P->nt;
   a.gdev = gdev;
   a.mode = mode == kModeUpdate ? P->wd_mode : mode;
-  a.item_lo = (int64_t)((__int128)P->items * shard / nshards);
-  a.item_hi = (int64_t)((__int128)P->items * (shard + 1) / nshards);
+  a.item_lo = phx_boundary(P, shard, nshards);
+  a.item_hi = phx_boundary(P, shard + 1, nshards);
   if (a.item_lo >= a.item_hi) return;
   for (int s0 = 0; s0 < k; s0 += kPhxSeeds) {
     const int nb = std::min(kPhxSeeds, k - s0);
@@ -1310,6 +1348,28 @@ int fks_shard_census(const fks_tensor* t, int32_t nt, int32_t shard, int32_t nsh
   return guarded([&] {
     validate(t, nt);
     if (nshards < 1 || shard < 0 || shard >= nshards) throw Error(-FKS_EINVAL, "bad shard");
+    if (rocm_stream(t, nt)) {  // element runs of whole Philox rows (phx_boundary)
+      std::lock_guard<std::mutex> lk(g_cache_mu);
+      const PhxPlan* P = get_phx_plan(t, nt, nullptr);
+      const int64_t lo = phx_boundary(P, shard, nshards), hi = phx_boundary(P, shard + 1, nshards);
+      if (word_range) {
+        word_range[0] = phx_boundary_elem(P, lo);
+        word_range[1] = phx_boundary_elem(P, hi);
+      }
+      if (!written) return;
+      for (int i = 0; i < nt; i++) written[i] = 0;
+      int ti = 0;  // table entry -> tensor index: the non-empty, non-frozen tensors in order
+      for (int k = 0; k < P->nt; k++) {
+        while (t[ti].numel == 0 || (t[ti].flags & FKS_FROZEN)) ti++;
+        const PhxTensor& T = P->tab[k];
+        const int64_t a0 = std::max(lo, T.item0), a1 = std::min(hi, T.item0 + T.stride * ((T.numel - 1) / (4 * (int64_t)T.stride) + 1));
+        if (a1 > a0)
+          written[ti] = std::min<int64_t>(T.numel, 4 * ((a1 - T.item0) / T.stride) * (int64_t)T.stride) -
+                        std::min<int64_t>(T.numel, 4 * ((a0 - T.item0) / T.stride) * (int64_t)T.stride);
+        ti++;
+      }
+      return;
+    }
     Layout L = make_layout(t, nt);
     const BlockRange br = shard_blocks(L.stream_len, shard, nshards);
     clip_segments(L, br);
@@ -1412,12 +1472,14 @@ int fks_host_jump_window(uint64_t seed, int64_t block, uint32_t* out624) {
 
 int fks_device_selfcheck(int32_t which, uint64_t* result, void* workspace, size_t ws_bytes, void* stream) {
   return guarded([&] {
-    if (!result || which != FKS_CHECK_SQRT_DOMAIN) throw Error(-FKS_EINVAL, "bad arguments");
+    if (!result || (which != FKS_CHECK_SQRT_DOMAIN && which != FKS_CHECK_PHILOX_RADIUS))
+      throw Error(-FKS_EINVAL, "bad arguments");
     const size_t need = sizeof(uint32_t) * (size_t)kSqrtDomainBlocks;
     if (!workspace || ws_bytes < need) throw Error(-FKS_EINVAL, "workspace too small");
     uint32_t* counts = static_cast<uint32_t*>(workspace);
-    int rc = launch_sqrt_domain_check(counts, stream);
-    if (rc) throw Error(-FKS_EHIP, std::string("sqrt domain check launch: ") + hipGetErrorString((hipError_t)rc));
+    int rc = which == FKS_CHECK_SQRT_DOMAIN ? launch_sqrt_domain_check(counts, stream)
+                                            : launch_philox_radius_check(counts, stream);
+    if (rc) throw Error(-FKS_EHIP, std::string("self check launch: ") + hipGetErrorString((hipError_t)rc));
     std::vector<uint32_t> h((size_t)kSqrtDomainBlocks);
     if (hipMemcpyAsync(h.data(), counts, need, hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
         hipStreamSynchronize((hipStream_t)stream) != hipSuccess)

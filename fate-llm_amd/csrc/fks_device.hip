@@ -1981,6 +1981,61 @@ __device__ __forceinline__ float phx_cast(float v) {  // static_cast<scalar_t>(f
   return DT == FKS_F32 ? v : Traits<DT>::rnd(v);
 }
 
+// Both Box-Muller pairs of one Philox output, (w.x, w.y) and (w.z, w.w), as the
+// instructions rocrand_box_muller compiles to, restricted to the inputs Philox can give
+// them and with the two pairs' float arithmetic packed (v_pk_*_f32):
+//   u = fma(x, 2^-32, 2^-32) lies in [2^-32, 1]: ocml's logf takes its normal-input path
+//     -- v_log_f32, then y ln2 in extended precision, r + e with r = RN(y ln2_hi),
+//     e = fma(y, ln2_hi, -r) + y ln2_lo -- with no denormal rescaling and no infinity
+//     select; the -2 (an exact scaling) is folded into ln2_hi / ln2_lo (RN(-2 a) = -2 RN(a)
+//     without underflow; only the sign of a zero can change, and a zero radius becomes +0
+//     in the final "+ 0" either way);
+//   x = -2 log u is 0 or >= 1.19e-7: the correctly rounded sqrtf takes its unscaled path
+//     -- v_sqrt_f32 and the +-1 ulp correction by two fma residuals (sqrt(+-0) = +-0
+//     falls out of the correction unchanged, so the +-0 / inf class select is dead);
+//   (sin(v) s, cos(v) s) + 0 as one fma with a +0 addend (no product underflows: |s| >=
+//     3.4e-4 or s = 0, |sin|, |cos| >= 1e-9 or exactly 0).
+// fks_device_selfcheck(FKS_CHECK_PHILOX_RADIUS) compares phx_radius2 with ocml's
+// sqrtf(-2 logf(u)) on all 2^32 words; tests/test_gpu_torch_rocm.py the whole stream with
+// torch.normal on the device.
+__device__ __forceinline__ f32x2_t phx_radius2(const f32x2_t u) {
+  const f32x2_t y = {__builtin_amdgcn_logf(u.x), __builtin_amdgcn_logf(u.y)};
+  const f32x2_t m2hi = {__uint_as_float(0xbfb17217u), __uint_as_float(0xbfb17217u)};  // -2 x 0x3f317217
+  const f32x2_t m2lo = {__uint_as_float(0xb3f7d1cfu), __uint_as_float(0xb3f7d1cfu)};  // -2 x 0x3377d1cf
+  const f32x2_t r = y * m2hi;
+  f32x2_t e = __builtin_elementwise_fma(y, m2hi, -r);
+  e = __builtin_elementwise_fma(m2lo, y, e);
+  const f32x2_t x = r + e;
+  f32x2_t sq = {__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
+  const f32x2_t sm = {__int_as_float(__float_as_int(sq.x) - 1), __int_as_float(__float_as_int(sq.y) - 1)};
+  const f32x2_t sp = {__int_as_float(__float_as_int(sq.x) + 1), __int_as_float(__float_as_int(sq.y) + 1)};
+  const f32x2_t rm = __builtin_elementwise_fma(-sm, sq, x), rp = __builtin_elementwise_fma(-sp, sq, x);
+  sq.x = rm.x <= 0.0f ? sm.x : sq.x;
+  sq.y = rm.y <= 0.0f ? sm.y : sq.y;
+  sq.x = rp.x > 0.0f ? sp.x : sq.x;
+  sq.y = rp.y > 0.0f ? sp.y : sq.y;
+  return sq;
+}
+
+__device__ __forceinline__ void phx_box_muller2(const uint4 w, f32x2_t& zA, f32x2_t& zB) {
+  const f32x2_t cu = {2.3283064e-10f, 2.3283064e-10f}, cv = {1.46291807e-09f, 1.46291807e-09f};
+  const f32x2_t fx = {(float)w.x, (float)w.z}, fy = {(float)w.y, (float)w.w};
+  const f32x2_t sq = phx_radius2(__builtin_elementwise_fma(fx, cu, cu));
+  const f32x2_t v = __builtin_elementwise_fma(fy, cv, cv);
+  const f32x2_t rev = v * (f32x2_t){__uint_as_float(0x3e22f983u), __uint_as_float(0x3e22f983u)};  // 1/(2 pi)
+  const f32x2_t sc1 = {__builtin_amdgcn_sinf(rev.x), __builtin_amdgcn_cosf(rev.x)};
+  const f32x2_t sc2 = {__builtin_amdgcn_sinf(rev.y), __builtin_amdgcn_cosf(rev.y)};
+  const f32x2_t zero = {0.0f, 0.0f};
+  zA = __builtin_elementwise_fma(sc1, (f32x2_t){sq.x, sq.x}, zero);
+  zB = __builtin_elementwise_fma(sc2, (f32x2_t){sq.y, sq.y}, zero);
+}
+
+// the radius of one word as ocml computes it (the reference's instructions), for the
+// self check of phx_radius2
+__device__ __forceinline__ float phx_radius_ocml(uint32_t x) {
+  return sqrtf(-2.0f * logf(__fmaf_rn((float)x, 2.3283064e-10f, 2.3283064e-10f)));
+}
+
 // The item's four elements through every seed of the pass, in seed order, as two packed
 // pairs (apply_pair: the values of apply_one); MODE may be a launch-wide weight-decay
 // specialisation of kModeUpdate (kModeUpdateWd / NoWd / Wd0, as the CPU stream's kernels).
@@ -2009,8 +2064,15 @@ __device__ __forceinline__ void phx_item(const PhiloxArgs& a, const PhxTensor& T
     const uint64_t seed = a.seeds[k];  // wave-uniform: scalar loads
     const float g = dv ? gd : a.g[3 * k + DT];
     const uint4 w = philox4x32_10(r1, seed);
+#if FKS_PHX_V1  // round-3 form (A/B): ocml's general logf / sqrtf and one pair at a time
     const float2 b1 = rocrand_box_muller(w.x, w.y), b2 = rocrand_box_muller(w.z, w.w);
     const f32x2_t zA = {phx_cast<DT>(b1.x), phx_cast<DT>(b1.y)}, zB = {phx_cast<DT>(b2.x), phx_cast<DT>(b2.y)};
+#else
+    f32x2_t zA, zB;
+    phx_box_muller2(w, zA, zB);
+    zA = (f32x2_t){phx_cast<DT>(zA.x), phx_cast<DT>(zA.y)};
+    zB = (f32x2_t){phx_cast<DT>(zB.x), phx_cast<DT>(zB.y)};
+#endif
     if (MODE == kModeWriteZ) {
       pA = zA;
       pB = zB;
@@ -2289,6 +2351,36 @@ __global__ __launch_bounds__(256) void fks_sqrt_domain_kernel(uint32_t* counts) 
   if (!ok) atomicAdd(&bad, 1u);
   __syncthreads();
   if (threadIdx.x == 0) counts[blockIdx.x] = bad;
+}
+
+// Device self check FKS_CHECK_PHILOX_RADIUS: the torch_rocm stream's radius
+// (phx_radius2, the trimmed logf + correctly rounded sqrtf) against ocml's general
+// sqrtf(-2 logf(u)) -- the reference's instructions -- on every one of the 2^32 Philox
+// words, bit for bit except the sign of a zero radius (the "+ 0" that follows erases
+// it).  kSqrtDomainBlocks workgroups of 256, 256 words per thread, one count each.
+__global__ __launch_bounds__(256) void fks_philox_radius_kernel(uint32_t* counts) {
+  __shared__ uint32_t bad;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  uint32_t n = 0;
+  const uint32_t base = (blockIdx.x * 256u + threadIdx.x) * 256u;
+  for (uint32_t i = 0; i < 256u; i += 2) {
+    const uint32_t x0 = base + i, x1 = base + i + 1;
+    const f32x2_t u = {__fmaf_rn((float)x0, 2.3283064e-10f, 2.3283064e-10f),
+                       __fmaf_rn((float)x1, 2.3283064e-10f, 2.3283064e-10f)};
+    const f32x2_t s = phx_radius2(u);
+    const float r0 = phx_radius_ocml(x0), r1 = phx_radius_ocml(x1);
+    n += (__float_as_uint(s.x + 0.0f) != __float_as_uint(r0 + 0.0f)) ? 1u : 0u;
+    n += (__float_as_uint(s.y + 0.0f) != __float_as_uint(r1 + 0.0f)) ? 1u : 0u;
+  }
+  if (n) atomicAdd(&bad, n);
+  __syncthreads();
+  if (threadIdx.x == 0) counts[blockIdx.x] = bad;
+}
+
+int launch_philox_radius_check(uint32_t* counts, void* stream) {
+  hipLaunchKernelGGL(fks_philox_radius_kernel, dim3(kSqrtDomainBlocks), dim3(256), 0, (hipStream_t)stream, counts);
+  return (int)hipGetLastError();
 }
 
 int launch_sqrt_domain_check(uint32_t* counts, void* stream) {

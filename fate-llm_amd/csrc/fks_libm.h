@@ -41,7 +41,20 @@ FKS_HD uint64_t bits(double x) { return __builtin_bit_cast(uint64_t, x); }
 FKS_HD double from_bits(uint64_t u) { return __builtin_bit_cast(double, u); }
 
 // glibc s_log1p.c (fdlibm): x = -u2 lies in (-1, 0], so the NaN / +inf / x >= 2^53 arms
-// of the original are unreachable and kept only as far as they are cheap.
+// of the original are unreachable and kept only as far as they are cheap.  The algorithm
+// and its constants are fdlibm's, whose notice follows:
+//
+//   ====================================================
+//   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+//
+//   Developed at SunPro, a Sun Microsystems, Inc. business.
+//   Permission to use, copy, modify, and distribute this
+//   software is freely granted, provided that this notice
+//   is preserved.
+//   ====================================================
+//
+// (glibc's dbl-64 s_log1p.c carries the same notice; its "modified by" changes -- the
+// split of the Lp polynomial evaluation -- are what the evaluation order below follows.)
 FKS_HD double log1p(double x) {
   FKS_NO_CONTRACT
   const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;

@@ -17,6 +17,7 @@ F32, BF16, F16 = 0, 1, 2
 HAS_WD, FROZEN, STREAM_ROCM = 1, 2, 4
 VALUE_SCALAR, VALUE_TENSOR = 0, 1
 CHECK_SQRT_DOMAIN = 1
+CHECK_PHILOX_RADIUS = 2
 ABI_VERSION = 1
 
 # every symbol include/fks.h declares (checked by tests/test_capi_host.py)

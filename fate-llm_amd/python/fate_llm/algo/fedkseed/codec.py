@@ -179,8 +179,13 @@ def directional_step(specs: Sequence[ParamSpec], seeds: Sequence[int], values: S
 # taken only while it stays within ZINDEX_BUDGET_FRAC of the device's memory (the
 # parameters' owner keeps the rest for activations); FKS_ZCACHE=0 turns it off.
 ZINDEX_BUDGET_FRAC = float(os.environ.get("FKS_ZINDEX_BUDGET_FRAC", "0.05"))
+ZINDEX_HEADROOM = 1 << 30  # free device memory the buffer always leaves untouched
 _zindex = {}  # device index -> attached uint8 tensor
 _zindex_lock = threading.Lock()
+
+
+def _alloc_zindex(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(nbytes, dtype=torch.uint8, device=device)
 
 
 def zindex_reserve(b: "_Batch") -> bool:
@@ -201,7 +206,17 @@ def zindex_reserve(b: "_Batch") -> bool:
             return True
         if need > ZINDEX_BUDGET_FRAC * torch.cuda.get_device_properties(idx).total_memory:
             return False
-        buf = torch.empty(need, dtype=torch.uint8, device=b.device)
+        # a speed cache only: never take the last of the device's memory for it (free memory
+        # as the driver sees it plus what torch holds cached and could hand out), and a
+        # failed allocation means "generate the z values", not an error
+        free, _ = torch.cuda.mem_get_info(idx)
+        reclaimable = torch.cuda.memory_reserved(idx) - torch.cuda.memory_allocated(idx)
+        if need > free + reclaimable - ZINDEX_HEADROOM:
+            return False
+        try:
+            buf = _alloc_zindex(need, b.device)
+        except torch.cuda.OutOfMemoryError:
+            return False
         N.check(L.fks_zindex_attach(buf.data_ptr(), need))  # waits for the old buffer's last user
         _zindex[idx] = buf
         return True
@@ -359,14 +374,16 @@ def delta_apply(specs: Sequence[ParamSpec], delta: torch.Tensor, decays: Sequenc
         b.finish()
 
 
-def shard_range(specs: Sequence[ParamSpec], shard: int, nshards: int):
-    """Stream words [lo, hi) that element shard ``shard`` of ``nshards`` owns
-    (fks_shard_census: the clipping fks_directional_step_shard launches with).  For a
-    list of contiguous tensors laid end to end whose sizes are multiples of 16 (no tail
-    recompute words) the words are the elements of their concatenation."""
-    b = _Batch(specs)
+def shard_range(specs: Sequence[ParamSpec], shard: int, nshards: int, stream_mode=None):
+    """What element shard ``shard`` of ``nshards`` owns (fks_shard_census: the clipping
+    fks_directional_step_shard launches with).  torch_cpu: the stream words [lo, hi); for
+    a list of contiguous tensors laid end to end whose sizes are multiples of 16 (no tail
+    recompute words) the words are the elements of their concatenation.  torch_rocm: the
+    elements [lo, hi) of the tensors' concatenation (runs of whole Philox rows)."""
+    b = _Batch(specs, stream_mode)
     rng = (ctypes.c_int64 * 2)()
-    N.check(N.load().fks_shard_census(ctypes.addressof(b.arr), b.n, int(shard), int(nshards), rng, None))
+    with torch.cuda.device(b.device):
+        N.check(N.load().fks_shard_census(ctypes.addressof(b.arr), b.n, int(shard), int(nshards), rng, None))
     return int(rng[0]), int(rng[1])
 
 

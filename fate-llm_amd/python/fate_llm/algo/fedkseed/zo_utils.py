@@ -143,7 +143,7 @@ def reconstruct_seed_sharded_(param_groups: List[dict], seeds: Sequence[int], va
     else:
         delta.zero_()
     codec.delta_accumulate(specs, [s for s, _ in keep[first:last]], coefs, delta)
-    if world > 1:
+    if distributed:  # also at world size 1: the group's collective library sums (an identity)
         dist.all_reduce(delta, op=dist.ReduceOp.SUM, group=process_group)
     codec.delta_apply(specs, delta, [decay] * len(specs))
     torch.manual_seed(keep[-1][0])

@@ -88,13 +88,15 @@ class FedKSeedRunner:
 
     @staticmethod
     def _training_args(conf: Dict, output_dir: Optional[str] = None):
-        from transformers import Seq2SeqTrainingArguments
+        """FATE's Seq2SeqTrainingArguments (trainer/seq2seq_trainer.py: no checkpoints,
+        constant lr, per-epoch logging, ...) as the reference runner builds them
+        (fedkseed_runner.py:95,120); the client's output dir is set afterwards (:97)."""
+        from fate_llm.trainer.seq2seq_trainer import Seq2SeqTrainingArguments
 
-        conf = dict(conf)
+        args = Seq2SeqTrainingArguments(**conf)
         if output_dir is not None:
-            conf["output_dir"] = output_dir
-        conf.setdefault("output_dir", "./")
-        return Seq2SeqTrainingArguments(**conf)
+            args.output_dir = output_dir
+        return args
 
     def client_setup(self, train_set=None, validate_set=None, output_dir=None, saved_model=None, stage="train"):
         if self.algo != "fedkseed":

@@ -107,11 +107,15 @@ int fks_directional_step_shard(const fks_tensor* t, int32_t nt, const uint64_t* 
                                int32_t k, int32_t value_kind, int32_t shard, int32_t nshards, void* workspace,
                                size_t ws_bytes, void* stream);
 
-/* Host-only census of element sharding (no device work): the stream words
+/* Census of element sharding (no kernel launch): the stream words
  * [word_range[0], word_range[1]) shard `shard` of `nshards` owns, and per tensor the
  * number of elements fks_directional_step_shard writes for it (`written`, nt entries;
  * either output may be NULL).  Over all shards every element of a non-frozen tensor
- * is written exactly once. */
+ * is written exactly once.  For FKS_STREAM_ROCM tensors the shards are runs of whole
+ * Philox rows (torch's grid-stride loop iterations: 4 x stride consecutive elements)
+ * and word_range is the shard's element range in the concatenation of all nt tensors
+ * (frozen and empty ones included); this builds (and caches) the call's tensor table
+ * on the current device. */
 int fks_shard_census(const fks_tensor* t, int32_t nt, int32_t shard, int32_t nshards, int64_t* word_range,
                      int64_t* written);
 
@@ -234,6 +238,12 @@ int fks_host_tables(int32_t dtype, float* radius, float* cosv, float* sinv, int3
  * values of u1 the reference can draw, checked against the exact midpoint criterion;
  * workspace >= 262,144 bytes. */
 #define FKS_CHECK_SQRT_DOMAIN 1
+/* FKS_CHECK_PHILOX_RADIUS: the torch_rocm stream's Box-Muller radius sqrt(-2 log u) as
+ * fks_philox_kernel computes it (trimmed to the inputs Philox can give) must equal
+ * ocml's general sqrtf(-2 logf(u)), the instructions torch's device kernel runs, on all
+ * 2^32 words (up to the sign of a zero, which the following "+ 0" erases); same
+ * workspace. */
+#define FKS_CHECK_PHILOX_RADIUS 2
 int fks_device_selfcheck(int32_t which, uint64_t* result, void* workspace, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus

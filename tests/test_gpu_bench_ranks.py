@@ -1,9 +1,10 @@
 """bench.py's multi-rank GPU path, rehearsed on a one-GPU box: `--gpus 2` re-launches the
 script under torch.distributed.run, both ranks run the codec on the visible GPU
 (FKS_BENCH_SHARE_GPU=1: they share it and talk over gloo instead of RCCL), each rank
-reconstructs its own buffer (--scaling weak, the default), its element shard (--scaling
-strong) or (--mode seed-shard) accumulates its seeds' delta and
-all-reduces it), rank 0 prints one JSON line with the world size the process group saw.
+reconstructs its element shard of one buffer (--scaling strong, the default), its own
+buffer (--scaling weak, opt-in, under its own metric name) or (--mode seed-shard)
+accumulates its seeds' delta and all-reduces it; rank 0 prints one JSON line with the
+world size the process group saw.
 The measured 8-GPU run is the driver's (one GPU per rank, RCCL)."""
 import json
 import os
@@ -17,8 +18,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("extra", [[], ["--scaling", "strong"], ["--scaling", "strong", "--gather"],
-                                   ["--mode", "seed-shard"]])
+@pytest.mark.parametrize("extra", [[], ["--scaling", "weak"], ["--gather"], ["--mode", "seed-shard"]])
 def test_bench_two_ranks_on_one_gpu(extra):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
@@ -33,8 +33,9 @@ def test_bench_two_ranks_on_one_gpu(extra):
     out = lines[0]
     assert out["n_gpus"] == 2 and out["backend"] == "gloo" and out["shared_gpu"]
     assert out["value"] > 0 and out["steps"] == 2
-    want = "seed-shard2" if "seed-shard" in extra else "element-shard2" if "strong" in extra else "client-per-gpu2"
+    want = "seed-shard2" if "seed-shard" in extra else "client-per-gpu2" if "weak" in extra else "element-shard2"
     assert out["config"]["parallelism"] == want
     assert out["scaling"] == ("weak" if want == "client-per-gpu2" else "strong")
+    assert out["metric"].endswith("[weak scaling: one buffer per GPU]") == (want == "client-per-gpu2")
     if "--gather" in extra:
         assert out["gather_ms"] > 0

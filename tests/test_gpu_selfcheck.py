@@ -26,6 +26,22 @@ def test_sqrt_domain_is_correctly_rounded():
     assert bad.value == 0
 
 
+def test_philox_radius_equals_ocml_on_all_words():
+    """The torch_rocm kernel's trimmed radius (phx_radius2) equals ocml's general
+    sqrtf(-2 logf(u)) -- what torch.normal runs on the device -- on all 2^32 words."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from fate_llm.algo.fedkseed import _native as N
+    L = N.load()
+    dev = torch.device("cuda", 0)
+    ws = torch.empty(1 << 18, dtype=torch.uint8, device=dev)
+    bad = ctypes.c_uint64(123)
+    with torch.cuda.device(dev):
+        N.check(L.fks_device_selfcheck(N.CHECK_PHILOX_RADIUS, ctypes.byref(bad), ws.data_ptr(), ws.numel(),
+                                       torch.cuda.current_stream(dev).cuda_stream))
+    assert bad.value == 0
+
+
 def test_selfcheck_rejects_bad_arguments():
     from fate_llm.algo.fedkseed import _native as N
     L = N.load()

@@ -145,6 +145,34 @@ def test_zindex_buffer_is_torch_memory_and_released():
     assert torch.equal(p.view(torch.int16), q.view(torch.int16))
 
 
+def test_zindex_skipped_when_memory_is_short_or_allocation_fails(monkeypatch):
+    """The z-index buffer is a speed cache: a device short of free memory (headroom
+    larger than what is free) or an allocation that raises OutOfMemoryError leaves it
+    unattached and the perturb generates its z -- same values, no error."""
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    codec.zindex_release()
+    p = torch.zeros(624 * 1000, dtype=torch.bfloat16, device=dev)
+    codec.perturb([p], 9, 1e-3)
+    codec.zindex_release()
+    q, r = torch.zeros_like(p), torch.zeros_like(p)
+    monkeypatch.setattr(codec, "ZINDEX_HEADROOM", 1 << 62)
+    before = torch.cuda.memory_allocated(dev)
+    codec.perturb([q], 9, 1e-3)
+    assert torch.cuda.memory_allocated(dev) - before < p.numel()
+    monkeypatch.setattr(codec, "ZINDEX_HEADROOM", 0)
+
+    def oom(nbytes, device):
+        raise torch.cuda.OutOfMemoryError("simulated")
+
+    monkeypatch.setattr(codec, "_alloc_zindex", oom)
+    assert codec.zindex_reserve(codec._Batch([codec.ParamSpec(r)])) is False
+    codec.perturb([r], 9, 1e-3)
+    torch.cuda.synchronize()
+    assert torch.equal(p.view(torch.int16), q.view(torch.int16))
+    assert torch.equal(p.view(torch.int16), r.view(torch.int16))
+
+
 @pytest.mark.parametrize("shape,dtype", [((1,), torch.float32), ((), torch.float64)])
 def test_device_tail_only_for_0dim_losses(shape, dtype):
     from fate_llm.algo.fedkseed.optimizer import ZerothOrderOptimizer

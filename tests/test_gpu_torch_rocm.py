@@ -116,3 +116,55 @@ def test_element_shards_equal_whole():
     torch.cuda.synchronize()
     for i, (a, b) in enumerate(zip(shards, whole)):
         _assert_same(a, b, f"tensor {i}")
+
+
+@pytest.mark.parametrize("nshards", [2, 3, 8])
+def test_element_shards_are_contiguous_runs_census(nshards):
+    """Element shards of the torch_rocm stream are runs of whole Philox rows: each shard
+    writes exactly the contiguous element range fks_shard_census reports for it (in the
+    tensors' concatenation, frozen and empty tensors included), the ranges tile the
+    buffer, and the per-tensor counts add up -- what bench.py --gather broadcasts."""
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    g = torch.Generator().manual_seed(13)
+    sizes = [4096, 48, 0, 9_000_017, 17_000, 700_001, 9]
+    frozen = [False, False, False, False, True, False, False]
+    total = sum(sizes)
+    flat0 = (torch.randn(total, generator=g) * 0.02).to(torch.bfloat16).to(dev)
+    seeds = torch.randint(0, 2**32, (3,), generator=g).tolist()
+    vals = (torch.randn(3, generator=g, dtype=torch.float64) * 20).tolist()
+
+    def specs(flat):
+        out, off = [], 0
+        for n, fz in zip(sizes, frozen):
+            out.append(codec.ParamSpec(flat[off:off + n], lr=1e-3, weight_decay=None, frozen=fz))
+            off += n
+        return out
+
+    whole = flat0.clone()
+    codec.directional_step(specs(whole), seeds, vals, stream_mode="torch_rocm")
+    ends, counts = [0], [0] * len(sizes)
+    for r in range(nshards):
+        one = flat0.clone()
+        sp = specs(one)
+        b = codec._Batch(sp, "torch_rocm")
+        import ctypes
+        from fate_llm.algo.fedkseed import _native as N
+        rng = (ctypes.c_int64 * 2)()
+        wr = (ctypes.c_int64 * len(sizes))()
+        N.check(N.load().fks_shard_census(ctypes.addressof(b.arr), b.n, r, nshards, rng, wr))
+        lo, hi = int(rng[0]), int(rng[1])
+        assert lo == ends[-1] and hi >= lo
+        ends.append(hi)
+        assert codec.shard_range(sp, r, nshards, stream_mode="torch_rocm") == (lo, hi)
+        codec.directional_step(sp, seeds, vals, shard=r, nshards=nshards, stream_mode="torch_rocm")
+        torch.cuda.synchronize()
+        changed = (one.view(torch.int16) != flat0.view(torch.int16)).nonzero().flatten()
+        if changed.numel():
+            assert int(changed.min()) >= lo and int(changed.max()) < hi, (r, lo, hi)
+        # inside its range the shard equals the whole reconstruct, outside it is untouched
+        assert torch.equal(one[lo:hi].view(torch.int16), whole[lo:hi].view(torch.int16))
+        for i in range(len(sizes)):
+            counts[i] += int(wr[i])
+    assert ends[-1] == total
+    assert counts == [0 if fz else n for n, fz in zip(sizes, frozen)]

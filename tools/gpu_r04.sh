@@ -1,0 +1,58 @@
+#!/bin/bash
+# Round-4 GPU driver: one parameterised script instead of per-experiment one-offs.
+#   tools/gpu_r04.sh TAG STEP [STEP ...]
+# STEP is one of
+#   pytest:<file[,file...]>     pytest -m gpu on those test files (tests/ prefix implied)
+#   pytestall                   the whole GPU suite
+#   rocm:<lib|intree>[:k]       tools/rocm_rate.py (torch_rocm stream, 7B bf16) on a build
+#   bench[:args]                bench.py with comma-separated extra args
+#   ubench:<name>               tools/ubench/<name>
+#   py:<script>[:args]          python tools/<script> with comma-separated args
+# Every GPU step runs under its own timeout; the first failing step ends the script.
+set -o pipefail
+TAG=$1
+shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+n=0
+for step in "$@"; do
+  n=$((n + 1))
+  kind=${step%%:*}
+  arg=${step#*:}
+  [ "$arg" = "$step" ] && arg=""
+  log="$OUT/$(printf %02d $n)_${kind}.log"
+  echo "[$TAG] step $n: $step -> $log"
+  case $kind in
+    pytest)
+      files=$(echo "$arg" | tr ',' ' ' | sed -e 's#\([^ ]*\)#tests/\1#g')
+      timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu $files > "$log" 2>&1 ;;
+    pytestall)
+      timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > "$log" 2>&1 ;;
+    rocm)
+      lib=${arg%%:*}
+      k=${arg#*:}
+      [ "$k" = "$arg" ] && k=64
+      if [ "$lib" = intree ]; then
+        timeout -k 10 300 python -u tools/rocm_rate.py --ref-seeds 0 --modes torch_rocm --k "$k" > "$log" 2>&1
+      else
+        FKS_LIB_OVERRIDE=$lib timeout -k 10 300 python -u tools/rocm_rate.py --ref-seeds 0 --modes torch_rocm --k "$k" > "$log" 2>&1
+      fi ;;
+    bench)
+      timeout -k 10 600 python -u bench.py $(echo "$arg" | tr ',' ' ') > "$log" 2>&1 ;;
+    ubench)
+      timeout -k 10 300 "tools/ubench/$arg" > "$log" 2>&1 ;;
+    py)
+      script=${arg%%:*}
+      a=${arg#*:}
+      [ "$a" = "$arg" ] && a=""
+      timeout -k 10 900 python -u "tools/$script" $(echo "$a" | tr ',' ' ') > "$log" 2>&1 ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+  rc=$?
+  tail -3 "$log"
+  if [ $rc -ne 0 ]; then
+    echo "[$TAG] step $n failed rc=$rc"
+    exit $rc
+  fi
+done

@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--k", type=int, default=64)
     ap.add_argument("--ref-seeds", type=int, default=3)
     ap.add_argument("--wd", type=float, default=0.0)
+    ap.add_argument("--modes", default="torch_rocm,torch_cpu", help="drop-in streams to time")
     args = ap.parse_args()
     from fate_llm.algo.fedkseed import codec
     dev = torch.device("cuda", 0)
@@ -60,19 +61,22 @@ def main():
     out = {"params": total, "dtype": "bf16", "weight_decay": args.wd, "lr": 1e-5}
 
     # the reference's loop on the GPU (its own torch calls), first seed as warm-up
-    reference_step(params, seeds[0], vals[0], 1e-5, args.wd)
-    t = timed(lambda: [reference_step(params, s, v, 1e-5, args.wd)
-                       for s, v in zip(seeds[1:1 + args.ref_seeds], vals[1:1 + args.ref_seeds])])
-    ref_s = t / args.ref_seeds
-    out["reference_gpu_torch"] = {"s_per_seed": round(ref_s, 5), "seeds_timed": args.ref_seeds,
-                                  "reconstruct_4055_seeds_s": round(ref_s * 4055, 1)}
+    ref_s = None
+    if args.ref_seeds > 0:
+        reference_step(params, seeds[0], vals[0], 1e-5, args.wd)
+        t = timed(lambda: [reference_step(params, s, v, 1e-5, args.wd)
+                           for s, v in zip(seeds[1:1 + args.ref_seeds], vals[1:1 + args.ref_seeds])])
+        ref_s = t / args.ref_seeds
+        out["reference_gpu_torch"] = {"s_per_seed": round(ref_s, 5), "seeds_timed": args.ref_seeds,
+                                      "reconstruct_4055_seeds_s": round(ref_s * 4055, 1)}
+    out["lib"] = os.environ.get("FKS_LIB_OVERRIDE", "libfks.so")
     specs = [codec.ParamSpec(p, lr=1e-5, weight_decay=args.wd) for p in params]
-    for mode in ("torch_rocm", "torch_cpu"):
+    for mode in args.modes.split(","):
         codec.directional_step(specs, seeds[:20], vals[:20], stream_mode=mode)  # plans, warm-up
         t = timed(lambda: codec.directional_step(specs, seeds, vals, stream_mode=mode))
         out[mode] = {"s_per_seed": round(t / args.k, 5), "k": args.k,
                      "reconstruct_4055_seeds_s": round(t / args.k * 4055, 2),
-                     "vs_reference_gpu": round(ref_s / (t / args.k), 2)}
+                     "vs_reference_gpu": round(ref_s / (t / args.k), 2) if ref_s else None}
     print(json.dumps(out), flush=True)
 
 
