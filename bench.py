@@ -71,6 +71,8 @@ VALU_MIX_CEILING_TLANEOPS = 1024 * 64 * 2.4e9 / VALU_MIX_CYCLES / 1e12
 # per-launch counters of the bf16 slice kernel (fks_apply_bs_kernel), tools/summarize_pmc2.py: the
 # weight-decay chain (wd != 0) and the zero-weight-decay chain (kModeUpdateWd0)
 PMC_SUMMARIES = {"wd": "pmc_apply_r03h_full.json", "wd0": "pmc_apply_r03h_wd0.json"}
+# the torch_rocm stream's kernel (fks_philox_kernel, 32-seed launches) at wd 0.0
+PMC_SUMMARY_PHX = "pmc_apply_r04c_phx_wd0.json"
 
 
 def llama7b_shapes():
@@ -106,14 +108,46 @@ def pmc_summary_name(wd):
     return PMC_SUMMARIES["wd0" if wd == 0.0 else "wd"]
 
 
-def load_pmc_summary(wd):
+def load_pmc_summary(wd=None, name=None):
     """Per-launch counters of the dominant kernel from the committed rocprofv3 --pmc
     passes (profiles/PMC_SUMMARIES, written by tools/summarize_pmc2.py)."""
     try:
-        with open(os.path.join(ROOT, "profiles", pmc_summary_name(wd))) as f:
+        with open(os.path.join(ROOT, "profiles", name or pmc_summary_name(wd))) as f:
             return json.load(f)
     except OSError:
         return {}
+
+
+def alt_stream_leg(codec, views, ks, kv, wd, total, build_id):
+    """The same 7B reconstruct drawn from the torch_rocm stream -- the z a reference client
+    draws when its model sits on an MI355X (zo_utils.py:47: device=param.data.device) --
+    timed once, with the VALU roofline of its kernel (fks_philox_kernel)."""
+    specs = [codec.ParamSpec(v, lr=1e-5, weight_decay=wd) for v in views]
+    codec.directional_step(specs, ks[:32], kv[:32], stream_mode="torch_rocm")  # the tensor table
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with codec.profile() as prof:
+        codec.directional_step(specs, ks, kv, stream_mode="torch_rocm")
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out = {"stream": "torch_rocm", "kernel": "fks_philox_kernel", "weight_decay": wd, "steps": 1,
+           "ms_per_step": round(dt * 1e3, 1), "value": round(total * 2 / dt / 1e9, 4), "unit": "GB/s",
+           "ms_per_seed": round(dt * 1e3 / len(ks), 3), "launches": prof.n_apply,
+           "kernel_ms": round(prof.apply_ms, 1)}
+    pmc = load_pmc_summary(name=PMC_SUMMARY_PHX)
+    lane_ops = pmc.get("valu_lane_ops_per_seed_param")
+    if lane_ops and pmc.get("build_id") == build_id and wd == 0.0:
+        ach = total * len(ks) * lane_ops / (prof.apply_ms / 1e3) / 1e12
+        out["roofline"] = {"bound": "valu", "achieved": round(ach, 3), "peak": round(VALU_PEAK_TLANEOPS, 2),
+                           "unit": "Tlane-op/s", "frac": round(ach / VALU_PEAK_TLANEOPS, 4),
+                           "lane_ops_per_unit": round(lane_ops, 3), "build_id": build_id,
+                           "counters": {k: pmc.get(k) for k in ("valu_active_frac", "clock_ghz")},
+                           "unit_def": f"one seed*param update; lane-ops from profiles/{PMC_SUMMARY_PHX}"}
+    else:
+        out["roofline"] = None
+        out["roofline_withheld"] = (f"profiles/{PMC_SUMMARY_PHX}: build {pmc.get('build_id')} / wd 0.0 only, "
+                                    f"this run build {build_id} wd {wd}")
+    return out
 
 
 # ------------------------------------------------------------------ CPU baseline
@@ -370,6 +404,12 @@ def run(args, world, rank, local):
         alt = {"weight_decay": args.alt_wd, "ms_per_step": round(alt_s * 1e3, 2),
                "value": round(total * 2 / alt_s / 1e9, 4), "steps": 1}
 
+    from fate_llm.algo.fedkseed import _native
+    build_id = _native.build_id()
+    alt_stream = None
+    if world == 1 and not seed_shard and args.alt_stream == "torch_rocm":
+        alt_stream = alt_stream_leg(codec, views, ks, kv, wd, total, build_id)
+
     ms_per_step = dt / args.steps * 1e3
     buf_bytes = total * 2 * (world if weak else 1)  # weak: one buffer per rank
     value = buf_bytes / (dt / args.steps) / 1e9
@@ -384,8 +424,6 @@ def run(args, world, rank, local):
     seeds_per_launch = rank_seeds * n_steps_prof / n_apply
     units = rank_params * seeds_per_launch  # seed*param updates per launch
     pmc = load_pmc_summary(wd)
-    from fate_llm.algo.fedkseed import _native
-    build_id = _native.build_id()
     lane_ops = pmc.get("valu_lane_ops_per_seed_param")
     valu = None
     withheld = None
@@ -470,6 +508,8 @@ def run(args, world, rank, local):
         out["gather_ms"] = round(gather_ms, 1)
     if alt is not None:
         out["alt_weight_decay"] = alt
+    if alt_stream is not None:
+        out["alt_stream"] = alt_stream
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_budget, wd)
     if rank == 0:
@@ -491,6 +531,9 @@ def main():
                          "reference's ClientTrainer passes, fedkseed.py:140; 'none' = zo_utils.py:52)")
     ap.add_argument("--alt-wd", type=lambda v: None if v == "none" else float(v), default=0.01,
                     help="N = 1: one more timed reconstruct at this weight decay, reported beside value")
+    ap.add_argument("--alt-stream", choices=("torch_rocm", "none"), default="torch_rocm",
+                    help="N = 1: one more timed reconstruct drawing the torch_rocm stream (a reference client "
+                         "whose model sits on the GPU), with its kernel's VALU roofline")
     ap.add_argument("--cpu-budget", type=float, default=24.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("sequential", "seed-shard"), default="sequential")

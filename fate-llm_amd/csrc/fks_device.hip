@@ -1953,7 +1953,8 @@ __device__ __forceinline__ uint4 philox4x32_10(const PhxRound1& r1, uint64_t see
 #pragma unroll
   for (int r = 1; r < 10; r++) {
     const uint64_t m0 = (uint64_t)0xD2511F53u * c0, m1 = (uint64_t)0xCD9E8D57u * c2;
-    const uint32_t n0 = (uint32_t)(m1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(m0 >> 32) ^ c3 ^ k1;
+    // one v_bitop3_b32 per three-input xor (two v_xor_b32 otherwise)
+    const uint32_t n0 = bs::xor3((uint32_t)(m1 >> 32), c1, k0), n2 = bs::xor3((uint32_t)(m0 >> 32), c3, k1);
     c1 = (uint32_t)m1;
     c3 = (uint32_t)m0;
     c0 = n0;

@@ -18,7 +18,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_LIB_PATH = os.environ.get("FKS_ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")  # override: sanitizer builds
 
 F32, BF16, F16, F64 = 0, 1, 2, 3
 DTYPE_NAMES = {"float32": F32, "bfloat16": BF16, "float16": F16, "float64": F64}

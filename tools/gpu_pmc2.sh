@@ -2,6 +2,9 @@
 # Round-2 PMC passes of the slice kernel for library variants, plus the issue2 ubench for
 # calibration (repo root on the GPU box):  VARIANTS="full cs0" bash tools/gpu_pmc2.sh
 # One rocprofv3 pass per counter group; results under gpurun_out/pmc2_<variant>_<group>/.
+# PERF_ARGS (tools/perf_one.py arguments), PERF_STREAM, PMC_SEEDS (seeds per launch) and
+# PMC_KERNEL (kernel-name substring for the summary) select another kernel, e.g. the
+# torch_rocm stream: PERF_STREAM=torch_rocm PMC_SEEDS=32 PMC_KERNEL=fks_philox_kernel.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 GROUPS_=("SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU2 SQ_INSTS_VALU GRBM_GUI_ACTIVE"
          "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_CVT SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 GRBM_GUI_ACTIVE"
@@ -20,7 +23,7 @@ for v in ${VARIANTS:-full}; do
   for g in "${GROUPS_[@]}"; do
     rm -rf gpurun_out/pmc2_${v}_$i
     timeout -s KILL 120 rocprofv3 --pmc $g -d gpurun_out/pmc2_${v}_$i -o run --output-format csv -- \
-      python3 tools/perf_one.py bf16 28 64 > gpurun_out/pmc2_${v}_$i.log 2>&1 || exit 99
+      python3 tools/perf_one.py ${PERF_ARGS:-bf16 28 64} > gpurun_out/pmc2_${v}_$i.log 2>&1 || exit 99
     i=$((i+1))
   done
 done
@@ -35,4 +38,4 @@ if [ -n "$UBENCH" ]; then
   done
 fi
 python3 tools/pmc2_show.py ${VARIANTS:-full}
-for v in ${VARIANTS:-full}; do python3 tools/summarize_pmc2.py "${TAG:-r02}_$v" $v $((1 << 28)) ${PMC_SEEDS:-64} > /dev/null; done
+for v in ${VARIANTS:-full}; do python3 tools/summarize_pmc2.py "${TAG:-r02}_$v" $v $((1 << 28)) ${PMC_SEEDS:-64} $PMC_KERNEL > /dev/null; done

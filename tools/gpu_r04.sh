@@ -8,6 +8,7 @@
 #   bench[:args]                bench.py with comma-separated extra args
 #   ubench:<name>               tools/ubench/<name>
 #   py:<script>[:args]          python tools/<script> with comma-separated args
+#   sh:<script>                 bash tools/<script> (environment passed through)
 # Every GPU step runs under its own timeout; the first failing step ends the script.
 set -o pipefail
 TAG=$1
@@ -46,6 +47,8 @@ for step in "$@"; do
       a=${arg#*:}
       [ "$a" = "$arg" ] && a=""
       timeout -k 10 900 python -u "tools/$script" $(echo "$a" | tr ',' ' ') > "$log" 2>&1 ;;
+    sh)
+      timeout -k 10 1200 bash "tools/$arg" > "$log" 2>&1 ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

@@ -1,6 +1,7 @@
 """One reconstruct of K seeds over an N-param buffer, twice, for kernel timing /
 counter collection (rocprofv3 around it).  python tools/perf_one.py [bf16|f32] [log2 N] [K]
-Defaults: bf16, N = 2^30, weight decay PERF_WD (default 0.01) (chunks as long as the 7B bench's order of magnitude), K = 19."""
+Defaults: bf16, N = 2^30, weight decay PERF_WD (default 0.01) (chunks as long as the 7B bench's order of magnitude), K = 19;
+PERF_STREAM=torch_rocm draws the torch_rocm stream (fks_philox_kernel)."""
 import os
 import sys
 
@@ -20,6 +21,6 @@ g = torch.Generator().manual_seed(1)
 seeds = torch.randint(0, 2**32, (k,), generator=g).tolist()
 vals = (torch.randn(k, generator=g, dtype=torch.float64) * 20).tolist()
 for _ in range(2):
-    codec.directional_step(specs, seeds, vals)
+    codec.directional_step(specs, seeds, vals, stream_mode=os.environ.get("PERF_STREAM", "torch_cpu"))
 torch.cuda.synchronize()
 print("done")

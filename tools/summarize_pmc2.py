@@ -65,7 +65,7 @@ def main(tag, variant, params, seeds, kernel=None, elt=2):
         "valu_dual_issue_frac": c.get("SQ_ACTIVE_INST_VALU2", 0.0) / c["SQ_INSTS_VALU"],
         "wait_any_frac": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"],
         "wait_inst_any_frac": c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"],
-        "lds_bank_conflict_frac": c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"],
+        "lds_bank_conflict_frac": (c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"] if c.get("SQ_LDS_IDX_ACTIVE") else None),
         "clock_cycles_per_launch": clk_cycles,
         # effective clock (MI355X_MICROARCH.md: GRBM_GUI_ACTIVE / 8 / wall time); profiled
         # passes run slightly slower than unprofiled ones
