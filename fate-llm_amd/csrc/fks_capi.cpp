@@ -4,6 +4,7 @@
 // Reference routines replaced (include/fks.h lists them): zo_utils.directional_derivative_step
 // (zo_utils.py:23-54), ZerothOrderOptimizer.random_perturb_parameters (optimizer.py:152-173),
 // and the per-seed reconstruct loop of ClientTrainer.train_once (fedkseed.py:136-141).
+#include <unordered_map>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -466,6 +467,7 @@ struct CachedPlan {
   uint64_t chunk_hash = 0;  // the chunk starts (regular + irregular): what a seed's windows depend on
   int64_t reg_lo = 0, reg_hi = 0;  // MT blocks [reg_lo, reg_hi) the regular chunks cover
   uint64_t bf16_hash = 0;  // the bf16 segments' stream ranges: which blocks a z-index store covers
+  uint64_t bs_hash = 0;    // the slice-kernel plan's chunk starts: what its seeds' windows depend on
 };
 
 // Table indices of the last one-seed bf16 perturb, per device (ZO step: the second and
@@ -506,12 +508,40 @@ struct WinCache {
   uint64_t seed = 0, chunk_hash = 0;
 };
 
+// The reconstruct window cache (fks_jwin_attach): the jumped windows of the slice
+// kernel's two-slice passes, per seed, in a CALLER-owned device buffer of window SETS
+// (one seed's windows at the pass's chunk-pair starts: nch x 624 words).  A client
+// reconstructs the same (seed, sum) list from model_0 every round (fedkseed.py:57-68:
+// the arbiter keeps the K seed candidates; :132-141), so the windows of one round are the
+// next round's: a seed found in the cache skips its jump.  Keyed by the plan's chunk
+// starts (bs_hash) -- another layout or shard resets it --; sets are recycled in
+// clock order, never one the current pass still needs.  Stream hand-off by event, as
+// WinCache.  Guarded by g_cache_mu.
+struct JWin {
+  int device = -1;
+  void* buf = nullptr;
+  size_t bytes = 0;
+  void* stream = nullptr;
+  hipEvent_t done = nullptr;
+  uint64_t key = 0;  // bs_hash of the plan the sets belong to (0: none)
+  int nch = 0;       // chunk pairs per set
+  uint32_t nsets = 0;
+  uint32_t clock = 0;
+  uint64_t pass = 0;                       // passes seen (stamps the sets a pass uses)
+  std::unordered_map<uint64_t, uint32_t> where;  // seed -> set
+  std::vector<uint64_t> set_seed;          // set -> seed (valid when set_used[s])
+  std::vector<uint8_t> set_used;
+  std::vector<uint64_t> set_pass;          // the last pass that used the set
+  uint64_t hits = 0, misses = 0;
+};
+
 constexpr size_t kPlanCacheEntries = 32;
 std::mutex g_cache_mu;
 std::vector<CachedPlan*> g_cache;
 uint64_t g_cache_clock = 0;
 std::vector<WinCache> g_win;
 std::vector<ZCache> g_zc;
+std::vector<JWin> g_jw;
 
 uint64_t fnv1a(const std::vector<uint8_t>& b) {
   uint64_t h = 1469598103934665603ull;
@@ -626,6 +656,9 @@ CachedPlan* build_plan(const fks_tensor* t, int nt, const double* scales, uint64
       key_put(bk, sg.numel);
     }
     C->bf16_hash = fnv1a(bk);
+    std::vector<uint8_t> sk;
+    for (int64_t b : BP.chunk_block) key_put(sk, b);
+    C->bs_hash = BP.chunk_block.empty() ? 0 : (fnv1a(sk) | 1u);
   }
   if (C->have_reg && !P.chunk_block.empty()) {
     C->reg_lo = P.chunk_block.front();
@@ -732,6 +765,13 @@ void clear_plan_cache() {
     Z.valid = false;
     Z.stream = nullptr;
   }
+  for (JWin& J : g_jw) {  // likewise
+    (void)hipSetDevice(J.device);
+    (void)hipDeviceSynchronize();
+    J.key = 0;
+    J.where.clear();
+    J.stream = nullptr;
+  }
   (void)hipSetDevice(cur);
   g_win.clear();
 }
@@ -766,6 +806,82 @@ ZCache* z_cache(void* stream, size_t bytes) {
   }
   Z->stream = stream;
   return Z;
+}
+
+// The reconstruct window cache entry of the current device (created on first use), or
+// nullptr if its event cannot be created.  Caller holds g_cache_mu.
+JWin* jw_entry() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  for (JWin& j : g_jw)
+    if (j.device == dev) return j.done ? &j : nullptr;
+  g_jw.emplace_back();
+  JWin* J = &g_jw.back();
+  J->device = dev;
+  if (hipEventCreateWithFlags(&J->done, hipEventDisableTiming) != hipSuccess) {
+    J->done = nullptr;
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return J;
+}
+
+// The reconstruct window cache for a call of the plan with bs_hash `key` and `nch` chunk
+// pairs on `stream`, ordered after its last user, or nullptr (none attached, or too small
+// for one two-slice pass).  A new key drops every set.
+JWin* jw_cache(void* stream, uint64_t key, int nch) {
+  if (std::getenv("FKS_NO_JWIN")) return nullptr;
+  JWin* J = jw_entry();
+  if (!J || !J->buf) return nullptr;
+  const size_t set_bytes = sizeof(uint32_t) * (size_t)kMtN * (size_t)nch;
+  const uint32_t nsets = (uint32_t)std::min<size_t>(J->bytes / set_bytes, UINT32_MAX);
+  if (nsets < (uint32_t)kBsPassSeeds) return nullptr;
+  if (J->stream && J->stream != stream) {
+    if (hipStreamWaitEvent((hipStream_t)stream, J->done, 0) != hipSuccess) return nullptr;
+  }
+  if (J->key != key || J->nch != nch || J->nsets != nsets) {
+    J->key = key;
+    J->nch = nch;
+    J->nsets = nsets;
+    J->clock = 0;
+    J->where.clear();
+    J->set_seed.assign(nsets, 0);
+    J->set_used.assign(nsets, 0);
+    J->set_pass.assign(nsets, 0);
+  }
+  J->stream = stream;
+  return J;
+}
+
+// Sets for the nb seeds of one two-slice pass: slot[j] = seed j's set; the seeds that
+// missed (their windows still to be jumped) are listed in miss / miss_slot.  A missing
+// seed takes the next set in clock order that this pass does not use.
+void jw_assign(JWin* J, const uint64_t* seeds, int nb, uint32_t* slot, uint64_t* miss, uint32_t* miss_slot,
+               int& nmiss) {
+  const uint64_t pass = ++J->pass;
+  nmiss = 0;
+  for (int j = 0; j < nb; j++) {
+    auto it = J->where.find(seeds[j]);
+    if (it != J->where.end()) {
+      slot[j] = it->second;
+      J->set_pass[it->second] = pass;
+      J->hits++;
+      continue;
+    }
+    uint32_t s = J->clock;
+    while (J->set_pass[s] == pass) s = (s + 1) % J->nsets;  // nsets >= 64 > nb: terminates
+    J->clock = (s + 1) % J->nsets;
+    if (J->set_used[s]) J->where.erase(J->set_seed[s]);
+    J->set_seed[s] = seeds[j];
+    J->set_used[s] = 1;
+    J->set_pass[s] = pass;
+    J->where[seeds[j]] = s;
+    slot[j] = s;
+    miss[nmiss] = seeds[j];
+    miss_slot[nmiss] = s;
+    nmiss++;
+    J->misses++;
+  }
 }
 
 // The window cache of the current device for a one-seed call on `stream` needing
@@ -1066,6 +1182,22 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
     int slices = 2;
     if (const char* e = std::getenv("FKS_BS_SLICES")) slices = (e[0] == '1') ? 1 : 2;
     const int per_pass = slices == 2 ? kBsPassSeeds : kBsSeeds;
+    // two-slice passes keep their windows in the reconstruct window cache when one is
+    // attached (fks_jwin_attach): a seed already there skips its jump
+    JWin* J = (slices == 2 && k > kBsSeeds) ? jw_cache(stream, C->bs_hash, C->Z.bs_chunks / kBsChunksPerWg) : nullptr;
+    struct JwOnThrow {  // a failed launch leaves sets assigned but not jumped: drop them all
+      JWin* J;
+      void* stream;
+      bool armed = true;
+      ~JwOnThrow() {
+        if (!J) return;
+        if (armed) {
+          J->key = 0;
+          J->where.clear();
+        }
+        (void)hipEventRecord(J->done, (hipStream_t)stream);
+      }
+    } jw_guard{J, stream};
     for (int s0 = 0; s0 < k; s0 += per_pass) {
       const int nb = std::min(per_pass, k - s0);
       // > 32 seeds: two slices per chunk pair (jumps to every other plan boundary);
@@ -1073,16 +1205,23 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
       const bool split = nb <= kBsSeeds;
       const int nch = split ? C->Z.bs_chunks : C->Z.bs_chunks / kBsChunksPerWg;
       JumpArgs ja{};
+      ApplyBsArgs ba{};
+      int njump = nb;
       for (int j = 0; j < nb; j++) ja.seeds[j] = seeds[s0 + j];
       ja.polys = reinterpret_cast<const uint64_t*>(hdr + C->H.off_bs_polys);
       ja.chunk_block = reinterpret_cast<const int64_t*>(hdr + C->H.off_bs_cb);
       ja.states = states;
+      ba.states = states;
+      if (J && !split) {
+        jw_assign(J, seeds + s0, nb, ba.slot, ja.seeds, ja.slot, njump);
+        ja.states = static_cast<uint32_t*>(J->buf);
+        ba.states = ja.states;
+        ja.use_slot = ba.use_slot = 1;
+      }
       ja.nchunks = nch;
       ja.stride = split ? 1 : kBsChunksPerWg;
-      ja.chunks_per_wg = std::max(1, std::min(nb * nch >= 4096 ? 32 : 16, nch));
-      check(timed(1, stream, [&] { return launch_jump(ja, nb, stream); }), "fks_jump_kernel");
-      ApplyBsArgs ba{};
-      ba.states = states;
+      ja.chunks_per_wg = std::max(1, std::min(njump * nch >= 4096 ? 32 : 16, nch));
+      if (njump > 0) check(timed(1, stream, [&] { return launch_jump(ja, njump, stream); }), "fks_jump_kernel");
       for (int j = 0; j < nb; j++) ba.g[j] = gval(s0 + j, FKS_BF16);
       ba.segs = reinterpret_cast<const DevSeg*>(hdr + C->seg_off[FKS_BF16]);
       ba.chunk_block = ja.chunk_block;
@@ -1094,6 +1233,7 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
       ba.mode = mode == kModeUpdate ? C->wd_mode[FKS_BF16] : mode;
       check(timed(0, stream, [&] { return launch_apply_bs(ba, stream); }), "fks_apply_bs_kernel");
     }
+    jw_guard.armed = false;
   }
   // the 19-seed kernels: every other regular dtype (all of them without the slice kernel)
   bool reg_rest = false;
@@ -1242,6 +1382,45 @@ int fks_zindex_attach(void* buf, size_t bytes) {
     Z->bytes = buf ? bytes : 0;
     Z->valid = false;
     Z->stream = nullptr;
+  });
+}
+
+int fks_jwin_size(const fks_tensor* t, int32_t nt, int32_t k, size_t* bytes) {
+  return guarded([&] {
+    validate(t, nt);
+    if (!bytes || k < 0) throw Error(-FKS_EINVAL, "bad arguments");
+    *bytes = 0;
+    if (rocm_stream(t, nt) || k <= kBsSeeds) return;  // the Philox stream jumps nothing
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    const CachedPlan* C = get_plan(t, nt, nullptr, 0, 0, 1, false);
+    if (!C->have_bs) return;
+    const size_t set_bytes = sizeof(uint32_t) * (size_t)kMtN * (size_t)(C->Z.bs_chunks / kBsChunksPerWg);
+    *bytes = set_bytes * (size_t)std::max(k, kBsPassSeeds);
+  });
+}
+
+int fks_jwin_attach(void* buf, size_t bytes) {
+  return guarded([&] {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    JWin* J = jw_entry();
+    if (!J) throw Error(-FKS_EHIP, "window cache event");
+    if (J->buf && J->stream && hipEventSynchronize(J->done) != hipSuccess)
+      throw Error(-FKS_EHIP, "window cache: waiting for the last user");
+    J->buf = bytes ? buf : nullptr;
+    J->bytes = buf ? bytes : 0;
+    J->key = 0;
+    J->where.clear();
+    J->stream = nullptr;
+  });
+}
+
+int fks_jwin_stats(uint64_t* hits, uint64_t* misses) {
+  return guarded([&] {
+    if (!hits || !misses) throw Error(-FKS_EINVAL, "bad arguments");
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    JWin* J = jw_entry();
+    *hits = J ? J->hits : 0;
+    *misses = J ? J->misses : 0;
   });
 }
 

@@ -349,7 +349,7 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
           }
         }
       }
-      uint32_t* out = a.states + ((size_t)k * a.nchunks + c) * kMtN + kW * lane;
+      uint32_t* out = a.states + ((size_t)(a.use_slot ? a.slot[k] : (uint32_t)k) * a.nchunks + c) * kMtN + kW * lane;
 #pragma unroll
       for (int j = 0; j < kW; j += 2)
         if (kW * lane + j < kMtN) *reinterpret_cast<uint2*>(out + j) = make_uint2(acc[j], acc[j + 1]);
@@ -699,6 +699,29 @@ __device__ __forceinline__ f32x2_t rnd2(f32x2_t x) {
   return r;
 }
 
+// The update modes' p-dependent part, given gz = rnd(g z): t = gz + rnd(wd p) (or the
+// form the launch's weight decay allows), p - rnd(lr t), each op rounded to the dtype.
+template <int DT, int MODE>
+__device__ __forceinline__ f32x2_t apply_tail(f32x2_t p, f32x2_t gz, float lr, float wd, bool has_wd) {
+  f32x2_t t;
+  if (MODE == kModeUpdateNoWd) {
+    t = gz;
+  } else if (MODE == kModeUpdateWd0) {
+    // wd = +-0: rnd(gz + rnd(wd*p)) == fma(wd, p, gz) (fks_internal.h)
+    const f32x2_t ww = {wd, wd};
+    t = __builtin_elementwise_fma(ww, p, gz);
+  } else {
+    const f32x2_t t2 = rnd2<DT>(gz + rnd2<DT>(wd * p));
+    if (MODE == kModeUpdateWd) {
+      t = t2;
+    } else {
+      t.x = has_wd ? t2.x : gz.x;
+      t.y = has_wd ? t2.y : gz.y;
+    }
+  }
+  return rnd2<DT>(p - rnd2<DT>(lr * t));
+}
+
 template <int DT, int MODE>
 __device__ __forceinline__ f32x2_t apply_pair(f32x2_t p, f32x2_t z, float g, float lr, float wd, bool has_wd,
                                               float ps, bool upd = true) {
@@ -711,26 +734,8 @@ __device__ __forceinline__ f32x2_t apply_pair(f32x2_t p, f32x2_t z, float g, flo
     if (MODE == kModePerturb || !upd) return p;
   }
   if (MODE == kModeUpdate || MODE == kModeUpdateWd || MODE == kModeUpdateNoWd || MODE == kModePerturbUpdate ||
-      MODE == kModeUpdateWd0) {
-    const f32x2_t gz = rnd2<DT>(g * z);
-    f32x2_t t;
-    if (MODE == kModeUpdateNoWd) {
-      t = gz;
-    } else if (MODE == kModeUpdateWd0) {
-      // wd = +-0: rnd(gz + rnd(wd*p)) == fma(wd, p, gz) (fks_internal.h)
-      const f32x2_t ww = {wd, wd};
-      t = __builtin_elementwise_fma(ww, p, gz);
-    } else {
-      const f32x2_t t2 = rnd2<DT>(gz + rnd2<DT>(wd * p));
-      if (MODE == kModeUpdateWd) {
-        t = t2;
-      } else {
-        t.x = has_wd ? t2.x : gz.x;
-        t.y = has_wd ? t2.y : gz.y;
-      }
-    }
-    return rnd2<DT>(p - rnd2<DT>(lr * t));
-  }
+      MODE == kModeUpdateWd0)
+    return apply_tail<DT, MODE>(p, rnd2<DT>(g * z), lr, wd, has_wd);
   return z;
 }
 
@@ -1499,7 +1504,9 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
     uint32_t w[32];
 #pragma unroll
     for (int k = 0; k < 32; k++)
-      w[k] = k < nseeds ? a.states[((size_t)(sfirst + k) * a.nchunks + c) * kMtN + i] : 0u;
+      w[k] = k < nseeds ? a.states[((size_t)(a.use_slot ? a.slot[sfirst + k] : (uint32_t)(sfirst + k)) * a.nchunks + c) *
+                                       kMtN + i]
+                        : 0u;
     bs::transpose32(w);
     bs_store_row(sbase + 16u * (uint32_t)i, w);
   }
@@ -1650,18 +1657,23 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
       p.x = ST::cvt(odd ? got : keep);
       p.y = ST::cvt(odd ? keep : got);
     }
+    auto z_of = [&](const int k) __attribute__((always_inline)) -> f32x2_t {
+      const float r = lds_f32(bs_index<2>(oa[k & 7], k >> 3));
+      const f32x2_t rr = {r, r}, zero = {0.0f, 0.0f};
+      const f32x2_t cs = lds_f32x2(1024u + bs_index<3>(ob[k & 7], k >> 3));
+      return rnd2<FKS_BF16>(__builtin_elementwise_fma(rr, cs, zero));
+    };
+    // (issuing seed k+1's lookups, z and g z ahead of seed k's p-dependent tail, which
+    // removes the wait state between the tail's dependent packed ops, measured 1 % slower:
+    // profiles/r04d_pipe_ab.log)
+    {
 #pragma unroll
-    for (int k = 0; k < kBsSeeds; k++) {
-      if (FULL || k < nseeds) {
-        const float r = lds_f32(bs_index<2>(oa[k & 7], k >> 3));
-        const f32x2_t rr = {r, r}, zero = {0.0f, 0.0f};
-        const f32x2_t cs = lds_f32x2(1024u + bs_index<3>(ob[k & 7], k >> 3));
-        const f32x2_t z = rnd2<FKS_BF16>(__builtin_elementwise_fma(rr, cs, zero));
-        p = apply_pair<FKS_BF16, MODE>(p, z, gk[k], sl.lr, sl.wd, sl.wdf != 0, 0.0f);
+      for (int k = 0; k < kBsSeeds; k++) {
+        if (FULL || k < nseeds) p = apply_pair<FKS_BF16, MODE>(p, z_of(k), gk[k], sl.lr, sl.wd, sl.wdf != 0, 0.0f);
+        // the lookups of one byte column (8 seeds) at a time: hoisting all 64 table reads
+        // ahead of the chain would spill
+        if ((k % kBsFence) == kBsFence - 1) asm volatile("" ::: "memory");
       }
-      // the lookups of one byte column (8 seeds) at a time: hoisting all 64 table reads
-      // ahead of the chain would spill
-      if ((k % kBsFence) == kBsFence - 1) asm volatile("" ::: "memory");
     }
     const uint32_t b1v = ST::bits(p.x), b2v = ST::bits(p.y);
     const uint32_t back = swap_adjacent(odd ? b1v : b2v);

@@ -178,6 +178,9 @@ struct ApplyBsArgs {
   int32_t nseeds;               // slices: 1..64, slice 0 takes seeds [0, ceil(n/2)), slice 1 the rest; split: 1..32
   int32_t mode;
   int32_t split;                // 1: one slice per plan chunk; 0: two slices on a chunk pair
+  int32_t use_slot;             // 1: seed k's windows are window set slot[k] of states (the
+                                // reconstruct window cache); 0: window set k
+  uint32_t slot[kBsPassSeeds];
 };
 
 struct JumpArgs {
@@ -188,6 +191,8 @@ struct JumpArgs {
   int32_t nchunks;
   int32_t chunks_per_wg;
   int32_t stride;               // chunk c starts at chunk_block[c * stride] (polys likewise); 0 = 1
+  int32_t use_slot;             // 1: seed k's windows go to window set slot[k] of states; 0: set k
+  uint32_t slot[kJumpMaxSeeds];
 };
 
 // ---- torch_rocm stream (FKS_STREAM_ROCM): torch.normal on a HIP device ----

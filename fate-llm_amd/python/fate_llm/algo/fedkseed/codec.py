@@ -146,12 +146,15 @@ def _seed_u64(s) -> int:
 
 
 def directional_step(specs: Sequence[ParamSpec], seeds: Sequence[int], values: Sequence[float],
-                     value_is_tensor: bool = False, shard: int = 0, nshards: int = 1, stream_mode=None) -> None:
+                     value_is_tensor: bool = False, shard: int = 0, nshards: int = 1, stream_mode=None,
+                     cache_windows: bool = False) -> None:
     """For each (seed, value) in order: p <- p - lr*(value*z + wd*p) over ``specs``.
 
     ``shard``/``nshards``: only the shard-th of nshards equal parts of the parameter stream
     is updated (element sharding across ranks; bit-identical): runs of MT19937 blocks
-    (torch_cpu) or of Philox work items (torch_rocm)."""
+    (torch_cpu) or of whole Philox rows (torch_rocm).  ``cache_windows``: keep the jumped
+    generator windows in the reconstruct window cache (jwin_reserve) so that the next
+    reconstruct of the same list skips the jumps of the seeds it finds there."""
     if len(seeds) != len(values):
         raise ValueError("seeds and values differ in length")
     if not specs or not len(seeds):
@@ -163,6 +166,8 @@ def directional_step(specs: Sequence[ParamSpec], seeds: Sequence[int], values: S
     s = np.ascontiguousarray([_seed_u64(x) for x in seeds], dtype=np.uint64)
     v = np.ascontiguousarray([float(x) for x in values], dtype=np.float64)
     with torch.cuda.device(b.device):
+        if cache_windows and b.stream_mode == "torch_cpu":
+            jwin_reserve(b, len(s))
         ws, nbytes = b.workspace(len(s))
         N.check(L.fks_directional_step_shard(ctypes.addressof(b.arr), b.n, s.ctypes.data, v.ctypes.data, len(s),
                                              N.VALUE_TENSOR if value_is_tensor else N.VALUE_SCALAR,
@@ -230,6 +235,68 @@ def zindex_release(device=None) -> None:
             with torch.cuda.device(idx):
                 N.check(L.fks_zindex_attach(None, 0))
             del _zindex[idx]
+
+
+# ---------------------------------------------------------------- reconstruct window cache
+# The generator windows a multi-seed bf16 reconstruct jumps to, one set per seed (include/
+# fks.h, fks_jwin_attach): a client reconstructs the same seed list from model_0 every
+# round, so from the second round on the jumps are skipped.  A torch tensor taken under
+# JWIN_BUDGET_FRAC of the device's memory and never past its free memory (less
+# ZINDEX_HEADROOM); an allocation failure only means "jump"; FKS_NO_JWIN=1 turns it off.
+JWIN_BUDGET_FRAC = float(os.environ.get("FKS_JWIN_BUDGET_FRAC", "0.05"))
+_jwin = {}  # device index -> attached uint8 tensor
+
+
+def _alloc_jwin(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(nbytes, dtype=torch.uint8, device=device)
+
+
+def jwin_reserve(b: "_Batch", k: int) -> bool:
+    """Attach a window cache that holds ``k`` seeds' window sets for the tensor list of
+    ``b`` on its device, if the budget allows; returns whether one is attached."""
+    if os.environ.get("FKS_NO_JWIN") or JWIN_BUDGET_FRAC <= 0:
+        return False
+    L = N.load()
+    need = ctypes.c_size_t(0)
+    N.check(L.fks_jwin_size(ctypes.addressof(b.arr), b.n, int(k), ctypes.byref(need)))
+    need = int(need.value)
+    if need == 0:
+        return False
+    idx = b.device.index if b.device.index is not None else torch.cuda.current_device()
+    with _zindex_lock:
+        cur = _jwin.get(idx)
+        if cur is not None and cur.numel() >= need:
+            return True
+        if need > JWIN_BUDGET_FRAC * torch.cuda.get_device_properties(idx).total_memory:
+            return False
+        free, _ = torch.cuda.mem_get_info(idx)
+        reclaimable = torch.cuda.memory_reserved(idx) - torch.cuda.memory_allocated(idx)
+        if need > free + reclaimable - ZINDEX_HEADROOM:
+            return False
+        try:
+            buf = _alloc_jwin(need, b.device)
+        except torch.cuda.OutOfMemoryError:
+            return False
+        N.check(L.fks_jwin_attach(buf.data_ptr(), need))  # waits for the old buffer's last user
+        _jwin[idx] = buf
+        return True
+
+
+def jwin_release(device=None) -> None:
+    """Detach and free the reconstruct window cache of ``device`` (all devices if None)."""
+    L = N.load()
+    with _zindex_lock:
+        for idx in [d for d in _jwin if device is None or d == torch.device(device).index]:
+            with torch.cuda.device(idx):
+                N.check(L.fks_jwin_attach(None, 0))
+            del _jwin[idx]
+
+
+def jwin_stats():
+    """(seeds found in the window cache, seeds jumped into it) since the library loaded."""
+    h, m = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    N.check(N.load().fks_jwin_stats(ctypes.byref(h), ctypes.byref(m)))
+    return int(h.value), int(m.value)
 
 
 def perturb(tensors: Sequence[torch.Tensor], seed: int, scales, stream_mode=None) -> None:

@@ -82,7 +82,10 @@ def reconstruct_(param_groups: List[dict], seeds: Sequence[int], values: Sequenc
     if not keep:
         return 0
     specs = codec.resolve_groups(param_groups, lr=lr, weight_decay=weight_decay)
-    codec.directional_step(specs, [s for s, _ in keep], [g for _, g in keep], value_is_tensor=False)
+    # the same list comes back every round (the arbiter's fixed seed candidates): keep the
+    # jumped generator windows for the next reconstruct (codec.jwin_reserve, a speed cache)
+    codec.directional_step(specs, [s for s, _ in keep], [g for _, g in keep], value_is_tensor=False,
+                           cache_windows=True)
     torch.manual_seed(keep[-1][0])  # the global generator was last seeded with the last applied seed
     return len(keep)
 

@@ -107,6 +107,22 @@ int fks_directional_step_shard(const fks_tensor* t, int32_t nt, const uint64_t* 
                                int32_t k, int32_t value_kind, int32_t shard, int32_t nshards, void* workspace,
                                size_t ws_bytes, void* stream);
 
+/* Reconstruct window cache (a speed cache, caller-owned like the z-index buffer): the
+ * generator windows a multi-seed bf16 reconstruct jumps to -- one window set of
+ * nchunk-pairs x 624 words per seed -- kept in `buf` on the current device, keyed by the
+ * seed and the plan's chunk starts, so that the next reconstruct of the same tensor list
+ * (or shard) skips the jumps of every seed it finds there.  A FedKSeed client rebuilds
+ * its model from model_0 and the same seed candidates every round
+ * (python/fate_llm/algo/fedkseed/fedkseed.py:57-68, :132-141), so from the second round
+ * on the reconstruct jumps nothing.  fks_jwin_size: bytes that hold k seeds' sets for
+ * this tensor list (0: the call would not use the cache); fks_jwin_attach: attach `buf`
+ * (bytes; NULL / 0 detaches), waiting for the last call that used the previous buffer;
+ * fks_jwin_stats: seeds found / jumped since the library loaded.  Calls on any stream
+ * are ordered by an event; fks_plan_cache_clear drops the contents. */
+int fks_jwin_size(const fks_tensor* t, int32_t nt, int32_t k, size_t* bytes);
+int fks_jwin_attach(void* buf, size_t bytes);
+int fks_jwin_stats(uint64_t* hits, uint64_t* misses);
+
 /* Census of element sharding (no kernel launch): the stream words
  * [word_range[0], word_range[1]) shard `shard` of `nshards` owns, and per tensor the
  * number of elements fks_directional_step_shard writes for it (`written`, nt entries;

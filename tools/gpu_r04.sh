@@ -9,6 +9,7 @@
 #   ubench:<name>               tools/ubench/<name>
 #   py:<script>[:args]          python tools/<script> with comma-separated args
 #   sh:<script>                 bash tools/<script> (environment passed through)
+#   ab:<lib|intree>[,<lib>...]  tools/ab_apply.py on those builds (AB_* environment)
 # Every GPU step runs under its own timeout; the first failing step ends the script.
 set -o pipefail
 TAG=$1
@@ -49,6 +50,8 @@ for step in "$@"; do
       timeout -k 10 900 python -u "tools/$script" $(echo "$a" | tr ',' ' ') > "$log" 2>&1 ;;
     sh)
       timeout -k 10 1200 bash "tools/$arg" > "$log" 2>&1 ;;
+    ab)
+      timeout -k 10 600 python -u tools/ab_apply.py $(echo "$arg" | tr ',' ' ' | sed -e 's#intree##g') > "$log" 2>&1 ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
