@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-4 GPU driver: one parameterised script instead of per-experiment one-offs.
-#   tools/gpu_r04.sh TAG STEP [STEP ...]
+# GPU driver: one parameterised script for every experiment (replaces the per-experiment one-offs).
+#   tools/gpu.sh TAG STEP [STEP ...]
 # STEP is one of
 #   pytest:<file[,file...]>     pytest -m gpu on those test files (tests/ prefix implied)
 #   pytestall                   the whole GPU suite
