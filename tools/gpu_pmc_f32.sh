@@ -9,6 +9,8 @@ GROUPS_=("SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTI
          "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT64 SQ_BUSY_CYCLES SQ_INST_LEVEL_LDS GRBM_GUI_ACTIVE"
          "FETCH_SIZE GRBM_GUI_ACTIVE"
          "WRITE_SIZE GRBM_GUI_ACTIVE")
+python3 -c 'import sys; sys.path.insert(0, "fate-llm_amd/python"); from fate_llm.algo.fedkseed import _native; print(_native.build_id())' \
+  > gpurun_out/pmc2_f32_buildid || exit 97
 i=0
 for g in "${GROUPS_[@]}"; do
   rm -rf gpurun_out/pmc2_f32_$i
