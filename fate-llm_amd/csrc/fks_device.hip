@@ -645,14 +645,10 @@ __device__ __forceinline__ void cephes_sincosf_nonneg(float x, float& s, float& 
 // domain -- x is +-0 or in [1.19e-7, 33.3], so the rescaling and class select are dead,
 // as phx_radius2 does for the Philox stream -- issues 14 % fewer VALU instructions in the
 // fp32 19-seed kernel but 50 % more hazard s_nops between its compares and selects, and
-// measured 3 % slower: profiles/r04h_sqrt_ab.log.)
-__device__ __forceinline__ float radius_sqrt(float x) {
-#if FKS_SQRT_F64  // A/B: v_sqrt_f64 rounded to f32 (no compares, no selects)
-  return (float)__builtin_amdgcn_sqrt((double)x);
-#else
-  return sqrtf(x);
-#endif
-}
+// measured 3 % slower: profiles/r04h_sqrt_ab.log.  v_sqrt_f64 rounded to f32 -- three
+// instructions, no select -- is 4.7 % faster but NOT correctly rounded: the self check
+// counts 1,326,243 of the 2^24 inputs wrong, profiles/r04i_sqrt64.log.)
+__device__ __forceinline__ float radius_sqrt(float x) { return sqrtf(x); }
 
 __device__ __forceinline__ void z_pair_f32_raw(uint32_t r1, uint32_t r2, float& z1, float& z2) {
   u32x2_t w;
