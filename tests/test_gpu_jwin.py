@@ -174,3 +174,35 @@ def test_full_size_shards_cold_and_warm(fresh_cache):
     codec.directional_step(spr, ks, kv, shard=3, nshards=8)
     torch.cuda.synchronize()
     assert torch.equal(_bits(buf), _bits(ref))
+
+
+def test_mixed_layout_cached_equals_uncached(fresh_cache):
+    """A list where the slice kernel's bf16 fast segments (cached windows) sit beside
+    tensors the other kernels take from the workspace's windows -- an fp32 tensor (19-seed
+    kernel), a ragged bf16 tensor and its unaligned successor (irregular kernel), an f16
+    tensor and numel < 16 tensors (serial path): cold and warm == uncached, bit for bit."""
+    codec = fresh_cache
+    dev = _dev()
+    g = torch.Generator().manual_seed(17)
+    spec = [((624 * 3000,), torch.bfloat16), ((5000, 3), torch.float32), ((1_000_003,), torch.bfloat16),
+            ((624 * 1000,), torch.bfloat16), ((7,), torch.bfloat16), ((4096, 4), torch.float16),
+            ((3,), torch.float32), ((624 * 2048,), torch.bfloat16)]
+    base = [(torch.randn(s, generator=g) * 0.02).to(dt).to(dev) for s, dt in spec]
+    ks, kv = _seeds(150, 18)
+
+    def run(cache, reps=1):
+        ps = [b.clone() for b in base]
+        sp = [codec.ParamSpec(p, lr=1e-3, weight_decay=0.01 if i % 2 else None) for i, p in enumerate(ps)]
+        for _ in range(reps):
+            codec.directional_step(sp, ks, kv, cache_windows=cache)
+        torch.cuda.synchronize()
+        return ps
+
+    ref = run(False, 2)
+    h0, m0 = codec.jwin_stats()
+    got = run(True, 2)  # the first call fills, the second finds every two-slice seed
+    h1, m1 = codec.jwin_stats()
+    for i, (a, b) in enumerate(zip(got, ref)):
+        w = torch.int16 if a.element_size() == 2 else torch.int32
+        assert torch.equal(a.view(w), b.view(w)), f"tensor {i}"
+    assert m1 - m0 == 128 and h1 - h0 == 128  # 2 two-slice passes of 64 seeds, then a 22-seed split pass
