@@ -265,6 +265,278 @@ __device__ __forceinline__ void jump_pair_step10(uint32_t (&acc)[10], uint32_t w
         [w7] "v"(w7), [w8] "v"(w8), [w9] "v"(w9), [w10] "v"(w10), [two] "s"(two)
       : "scc");
 }
+// acc[j] ^= XOR over the set bits d of the wave-uniform 4-bit code of w[d + j] (j < 10):
+// coefficients 4 at a time.  A binary tree of scalar bit tests picks one of 16 bodies
+// (none, one v_xor_b32, one v_bitop3_b32, or two of them per word), so a random polynomial
+// costs 1.25 VALU ops per word per 4 coefficients -- 0.3125 per coefficient against the
+// pair step's 0.375 -- and 4 scalar tests instead of 2 x (1-3) compares.
+__device__ __forceinline__ void jump_quad_step10(uint32_t (&acc)[10], const uint32_t (&w)[13], uint32_t code) {
+  asm volatile(
+      "s_bitcmp1_b32 %[c], 3\n"
+      "s_cbranch_scc1 .Lqb3k8x%=\n"
+      "s_bitcmp1_b32 %[c], 2\n"
+      "s_cbranch_scc1 .Lqb2k4x%=\n"
+      "s_bitcmp1_b32 %[c], 1\n"
+      "s_cbranch_scc1 .Lqb1k2x%=\n"
+      "s_bitcmp1_b32 %[c], 0\n"
+      "s_cbranch_scc1 .Lqb0k1x%=\n"
+      "s_branch .Lqendx%=\n"
+      ".Lqb0k1x%=:\n"
+      "v_xor_b32 %[a0], %[a0], %[w0]\n"
+      "v_xor_b32 %[a1], %[a1], %[w1]\n"
+      "v_xor_b32 %[a2], %[a2], %[w2]\n"
+      "v_xor_b32 %[a3], %[a3], %[w3]\n"
+      "v_xor_b32 %[a4], %[a4], %[w4]\n"
+      "v_xor_b32 %[a5], %[a5], %[w5]\n"
+      "v_xor_b32 %[a6], %[a6], %[w6]\n"
+      "v_xor_b32 %[a7], %[a7], %[w7]\n"
+      "v_xor_b32 %[a8], %[a8], %[w8]\n"
+      "v_xor_b32 %[a9], %[a9], %[w9]\n"
+      "s_branch .Lqendx%=\n"
+      ".Lqb1k2x%=:\n"
+      "s_bitcmp1_b32 %[c], 0\n"
+      "s_cbranch_scc1 .Lqb0k3x%=\n"
+      "v_xor_b32 %[a0], %[a0], %[w1]\n"
+      "v_xor_b32 %[a1], %[a1], %[w2]\n"
+      "v_xor_b32 %[a2], %[a2], %[w3]\n"
+      "v_xor_b32 %[a3], %[a3], %[w4]\n"
+      "v_xor_b32 %[a4], %[a4], %[w5]\n"
+      "v_xor_b32 %[a5], %[a5], %[w6]\n"
+      "v_xor_b32 %[a6], %[a6], %[w7]\n"
+      "v_xor_b32 %[a7], %[a7], %[w8]\n"
+      "v_xor_b32 %[a8], %[a8], %[w9]\n"
+      "v_xor_b32 %[a9], %[a9], %[w10]\n"
+      "s_branch .Lqendx%=\n"
+      ".Lqb0k3x%=:\n"
+      "v_bitop3_b32 %[a0], %[a0], %[w0], %[w1] bitop3:0x96\n"
+      "v_bitop3_b32 %[a1], %[a1], %[w1], %[w2] bitop3:0x96\n"
+      "v_bitop3_b32 %[a2], %[a2], %[w2], %[w3] bitop3:0x96\n"
+      "v_bitop3_b32 %[a3], %[a3], %[w3], %[w4] bitop3:0x96\n"
+      "v_bitop3_b32 %[a4], %[a4], %[w4], %[w5] bitop3:0x96\n"
+      "v_bitop3_b32 %[a5], %[a5], %[w5], %[w6] bitop3:0x96\n"
+      "v_bitop3_b32 %[a6], %[a6], %[w6], %[w7] bitop3:0x96\n"
+      "v_bitop3_b32 %[a7], %[a7], %[w7], %[w8] bitop3:0x96\n"
+      "v_bitop3_b32 %[a8], %[a8], %[w8], %[w9] bitop3:0x96\n"
+      "v_bitop3_b32 %[a9], %[a9], %[w9], %[w10] bitop3:0x96\n"
+      "s_branch .Lqendx%=\n"
+      ".Lqb2k4x%=:\n"
+      "s_bitcmp1_b32 %[c], 1\n"
+      "s_cbranch_scc1 .Lqb1k6x%=\n"
+      "s_bitcmp1_b32 %[c], 0\n"
+      "s_cbranch_scc1 .Lqb0k5x%=\n"
+      "v_xor_b32 %[a0], %[a0], %[w2]\n"
+      "v_xor_b32 %[a1], %[a1], %[w3]\n"
+      "v_xor_b32 %[a2], %[a2], %[w4]\n"
+      "v_xor_b32 %[a3], %[a3], %[w5]\n"
+      "v_xor_b32 %[a4], %[a4], %[w6]\n"
+      "v_xor_b32 %[a5], %[a5], %[w7]\n"
+      "v_xor_b32 %[a6], %[a6], %[w8]\n"
+      "v_xor_b32 %[a7], %[a7], %[w9]\n"
+      "v_xor_b32 %[a8], %[a8], %[w10]\n"
+      "v_xor_b32 %[a9], %[a9], %[w11]\n"
+      "s_branch .Lqendx%=\n"
+      ".Lqb0k5x%=:\n"
+      "v_bitop3_b32 %[a0], %[a0], %[w0], %[w2] bitop3:0x96\n"
+      "v_bitop3_b32 %[a1], %[a1], %[w1], %[w3] bitop3:0x96\n"
+      "v_bitop3_b32 %[a2], %[a2], %[w2], %[w4] bitop3:0x96\n"
+      "v_bitop3_b32 %[a3], %[a3], %[w3], %[w5] bitop3:0x96\n"
+      "v_bitop3_b32 %[a4], %[a4], %[w4], %[w6] bitop3:0x96\n"
+      "v_bitop3_b32 %[a5], %[a5], %[w5], %[w7] bitop3:0x96\n"
+      "v_bitop3_b32 %[a6], %[a6], %[w6], %[w8] bitop3:0x96\n"
+      "v_bitop3_b32 %[a7], %[a7], %[w7], %[w9] bitop3:0x96\n"
+      "v_bitop3_b32 %[a8], %[a8], %[w8], %[w10] bitop3:0x96\n"
+      "v_bitop3_b32 %[a9], %[a9], %[w9], %[w11] bitop3:0x96\n"
+      "s_branch .Lqendx%=\n"
+      ".Lqb1k6x%=:\n"
+      "s_bitcmp1_b32 %[c], 0\n"
+      "s_cbranch_scc1 .Lqb0k7x%=\n"
+      "v_bitop3_b32 %[a0], %[a0], %[w1], %[w2] bitop3:0x96\n"
+      "v_bitop3_b32 %[a1], %[a1], %[w2], %[w3] bitop3:0x96\n"
+      "v_bitop3_b32 %[a2], %[a2], %[w3], %[w4] bitop3:0x96\n"
+      "v_bitop3_b32 %[a3], %[a3], %[w4], %[w5] bitop3:0x96\n"
+      "v_bitop3_b32 %[a4], %[a4], %[w5], %[w6] bitop3:0x96\n"
+      "v_bitop3_b32 %[a5], %[a5], %[w6], %[w7] bitop3:0x96\n"
+      "v_bitop3_b32 %[a6], %[a6], %[w7], %[w8] bitop3:0x96\n"
+      "v_bitop3_b32 %[a7], %[a7], %[w8], %[w9] bitop3:0x96\n"
+      "v_bitop3_b32 %[a8], %[a8], %[w9], %[w10] bitop3:0x96\n"
+      "v_bitop3_b32 %[a9], %[a9], %[w10], %[w11] bitop3:0x96\n"
+      "s_branch .Lqendx%=\n"
+      ".Lqb0k7x%=:\n"
+      "v_bitop3_b32 %[a0], %[a0], %[w0], %[w1] bitop3:0x96\n"
+      "v_xor_b32 %[a0], %[a0], %[w2]\n"
+      "v_bitop3_b32 %[a1], %[a1], %[w1], %[w2] bitop3:0x96\n"
+      "v_xor_b32 %[a1], %[a1], %[w3]\n"
+      "v_bitop3_b32 %[a2], %[a2], %[w2], %[w3] bitop3:0x96\n"
+      "v_xor_b32 %[a2], %[a2], %[w4]\n"
+      "v_bitop3_b32 %[a3], %[a3], %[w3], %[w4] bitop3:0x96\n"
+      "v_xor_b32 %[a3], %[a3], %[w5]\n"
+      "v_bitop3_b32 %[a4], %[a4], %[w4], %[w5] bitop3:0x96\n"
+      "v_xor_b32 %[a4], %[a4], %[w6]\n"
+      "v_bitop3_b32 %[a5], %[a5], %[w5], %[w6] bitop3:0x96\n"
+      "v_xor_b32 %[a5], %[a5], %[w7]\n"
+      "v_bitop3_b32 %[a6], %[a6], %[w6], %[w7] bitop3:0x96\n"
+      "v_xor_b32 %[a6], %[a6], %[w8]\n"
+      "v_bitop3_b32 %[a7], %[a7], %[w7], %[w8] bitop3:0x96\n"
+      "v_xor_b32 %[a7], %[a7], %[w9]\n"
+      "v_bitop3_b32 %[a8], %[a8], %[w8], %[w9] bitop3:0x96\n"
+      "v_xor_b32 %[a8], %[a8], %[w10]\n"
+      "v_bitop3_b32 %[a9], %[a9], %[w9], %[w10] bitop3:0x96\n"
+      "v_xor_b32 %[a9], %[a9], %[w11]\n"
+      "s_branch .Lqendx%=\n"
+      ".Lqb3k8x%=:\n"
+      "s_bitcmp1_b32 %[c], 2\n"
+      "s_cbranch_scc1 .Lqb2k12x%=\n"
+      "s_bitcmp1_b32 %[c], 1\n"
+      "s_cbranch_scc1 .Lqb1k10x%=\n"
+      "s_bitcmp1_b32 %[c], 0\n"
+      "s_cbranch_scc1 .Lqb0k9x%=\n"
+      "v_xor_b32 %[a0], %[a0], %[w3]\n"
+      "v_xor_b32 %[a1], %[a1], %[w4]\n"
+      "v_xor_b32 %[a2], %[a2], %[w5]\n"
+      "v_xor_b32 %[a3], %[a3], %[w6]\n"
+      "v_xor_b32 %[a4], %[a4], %[w7]\n"
+      "v_xor_b32 %[a5], %[a5], %[w8]\n"
+      "v_xor_b32 %[a6], %[a6], %[w9]\n"
+      "v_xor_b32 %[a7], %[a7], %[w10]\n"
+      "v_xor_b32 %[a8], %[a8], %[w11]\n"
+      "v_xor_b32 %[a9], %[a9], %[w12]\n"
+      "s_branch .Lqendx%=\n"
+      ".Lqb0k9x%=:\n"
+      "v_bitop3_b32 %[a0], %[a0], %[w0], %[w3] bitop3:0x96\n"
+      "v_bitop3_b32 %[a1], %[a1], %[w1], %[w4] bitop3:0x96\n"
+      "v_bitop3_b32 %[a2], %[a2], %[w2], %[w5] bitop3:0x96\n"
+      "v_bitop3_b32 %[a3], %[a3], %[w3], %[w6] bitop3:0x96\n"
+      "v_bitop3_b32 %[a4], %[a4], %[w4], %[w7] bitop3:0x96\n"
+      "v_bitop3_b32 %[a5], %[a5], %[w5], %[w8] bitop3:0x96\n"
+      "v_bitop3_b32 %[a6], %[a6], %[w6], %[w9] bitop3:0x96\n"
+      "v_bitop3_b32 %[a7], %[a7], %[w7], %[w10] bitop3:0x96\n"
+      "v_bitop3_b32 %[a8], %[a8], %[w8], %[w11] bitop3:0x96\n"
+      "v_bitop3_b32 %[a9], %[a9], %[w9], %[w12] bitop3:0x96\n"
+      "s_branch .Lqendx%=\n"
+      ".Lqb1k10x%=:\n"
+      "s_bitcmp1_b32 %[c], 0\n"
+      "s_cbranch_scc1 .Lqb0k11x%=\n"
+      "v_bitop3_b32 %[a0], %[a0], %[w1], %[w3] bitop3:0x96\n"
+      "v_bitop3_b32 %[a1], %[a1], %[w2], %[w4] bitop3:0x96\n"
+      "v_bitop3_b32 %[a2], %[a2], %[w3], %[w5] bitop3:0x96\n"
+      "v_bitop3_b32 %[a3], %[a3], %[w4], %[w6] bitop3:0x96\n"
+      "v_bitop3_b32 %[a4], %[a4], %[w5], %[w7] bitop3:0x96\n"
+      "v_bitop3_b32 %[a5], %[a5], %[w6], %[w8] bitop3:0x96\n"
+      "v_bitop3_b32 %[a6], %[a6], %[w7], %[w9] bitop3:0x96\n"
+      "v_bitop3_b32 %[a7], %[a7], %[w8], %[w10] bitop3:0x96\n"
+      "v_bitop3_b32 %[a8], %[a8], %[w9], %[w11] bitop3:0x96\n"
+      "v_bitop3_b32 %[a9], %[a9], %[w10], %[w12] bitop3:0x96\n"
+      "s_branch .Lqendx%=\n"
+      ".Lqb0k11x%=:\n"
+      "v_bitop3_b32 %[a0], %[a0], %[w0], %[w1] bitop3:0x96\n"
+      "v_xor_b32 %[a0], %[a0], %[w3]\n"
+      "v_bitop3_b32 %[a1], %[a1], %[w1], %[w2] bitop3:0x96\n"
+      "v_xor_b32 %[a1], %[a1], %[w4]\n"
+      "v_bitop3_b32 %[a2], %[a2], %[w2], %[w3] bitop3:0x96\n"
+      "v_xor_b32 %[a2], %[a2], %[w5]\n"
+      "v_bitop3_b32 %[a3], %[a3], %[w3], %[w4] bitop3:0x96\n"
+      "v_xor_b32 %[a3], %[a3], %[w6]\n"
+      "v_bitop3_b32 %[a4], %[a4], %[w4], %[w5] bitop3:0x96\n"
+      "v_xor_b32 %[a4], %[a4], %[w7]\n"
+      "v_bitop3_b32 %[a5], %[a5], %[w5], %[w6] bitop3:0x96\n"
+      "v_xor_b32 %[a5], %[a5], %[w8]\n"
+      "v_bitop3_b32 %[a6], %[a6], %[w6], %[w7] bitop3:0x96\n"
+      "v_xor_b32 %[a6], %[a6], %[w9]\n"
+      "v_bitop3_b32 %[a7], %[a7], %[w7], %[w8] bitop3:0x96\n"
+      "v_xor_b32 %[a7], %[a7], %[w10]\n"
+      "v_bitop3_b32 %[a8], %[a8], %[w8], %[w9] bitop3:0x96\n"
+      "v_xor_b32 %[a8], %[a8], %[w11]\n"
+      "v_bitop3_b32 %[a9], %[a9], %[w9], %[w10] bitop3:0x96\n"
+      "v_xor_b32 %[a9], %[a9], %[w12]\n"
+      "s_branch .Lqendx%=\n"
+      ".Lqb2k12x%=:\n"
+      "s_bitcmp1_b32 %[c], 1\n"
+      "s_cbranch_scc1 .Lqb1k14x%=\n"
+      "s_bitcmp1_b32 %[c], 0\n"
+      "s_cbranch_scc1 .Lqb0k13x%=\n"
+      "v_bitop3_b32 %[a0], %[a0], %[w2], %[w3] bitop3:0x96\n"
+      "v_bitop3_b32 %[a1], %[a1], %[w3], %[w4] bitop3:0x96\n"
+      "v_bitop3_b32 %[a2], %[a2], %[w4], %[w5] bitop3:0x96\n"
+      "v_bitop3_b32 %[a3], %[a3], %[w5], %[w6] bitop3:0x96\n"
+      "v_bitop3_b32 %[a4], %[a4], %[w6], %[w7] bitop3:0x96\n"
+      "v_bitop3_b32 %[a5], %[a5], %[w7], %[w8] bitop3:0x96\n"
+      "v_bitop3_b32 %[a6], %[a6], %[w8], %[w9] bitop3:0x96\n"
+      "v_bitop3_b32 %[a7], %[a7], %[w9], %[w10] bitop3:0x96\n"
+      "v_bitop3_b32 %[a8], %[a8], %[w10], %[w11] bitop3:0x96\n"
+      "v_bitop3_b32 %[a9], %[a9], %[w11], %[w12] bitop3:0x96\n"
+      "s_branch .Lqendx%=\n"
+      ".Lqb0k13x%=:\n"
+      "v_bitop3_b32 %[a0], %[a0], %[w0], %[w2] bitop3:0x96\n"
+      "v_xor_b32 %[a0], %[a0], %[w3]\n"
+      "v_bitop3_b32 %[a1], %[a1], %[w1], %[w3] bitop3:0x96\n"
+      "v_xor_b32 %[a1], %[a1], %[w4]\n"
+      "v_bitop3_b32 %[a2], %[a2], %[w2], %[w4] bitop3:0x96\n"
+      "v_xor_b32 %[a2], %[a2], %[w5]\n"
+      "v_bitop3_b32 %[a3], %[a3], %[w3], %[w5] bitop3:0x96\n"
+      "v_xor_b32 %[a3], %[a3], %[w6]\n"
+      "v_bitop3_b32 %[a4], %[a4], %[w4], %[w6] bitop3:0x96\n"
+      "v_xor_b32 %[a4], %[a4], %[w7]\n"
+      "v_bitop3_b32 %[a5], %[a5], %[w5], %[w7] bitop3:0x96\n"
+      "v_xor_b32 %[a5], %[a5], %[w8]\n"
+      "v_bitop3_b32 %[a6], %[a6], %[w6], %[w8] bitop3:0x96\n"
+      "v_xor_b32 %[a6], %[a6], %[w9]\n"
+      "v_bitop3_b32 %[a7], %[a7], %[w7], %[w9] bitop3:0x96\n"
+      "v_xor_b32 %[a7], %[a7], %[w10]\n"
+      "v_bitop3_b32 %[a8], %[a8], %[w8], %[w10] bitop3:0x96\n"
+      "v_xor_b32 %[a8], %[a8], %[w11]\n"
+      "v_bitop3_b32 %[a9], %[a9], %[w9], %[w11] bitop3:0x96\n"
+      "v_xor_b32 %[a9], %[a9], %[w12]\n"
+      "s_branch .Lqendx%=\n"
+      ".Lqb1k14x%=:\n"
+      "s_bitcmp1_b32 %[c], 0\n"
+      "s_cbranch_scc1 .Lqb0k15x%=\n"
+      "v_bitop3_b32 %[a0], %[a0], %[w1], %[w2] bitop3:0x96\n"
+      "v_xor_b32 %[a0], %[a0], %[w3]\n"
+      "v_bitop3_b32 %[a1], %[a1], %[w2], %[w3] bitop3:0x96\n"
+      "v_xor_b32 %[a1], %[a1], %[w4]\n"
+      "v_bitop3_b32 %[a2], %[a2], %[w3], %[w4] bitop3:0x96\n"
+      "v_xor_b32 %[a2], %[a2], %[w5]\n"
+      "v_bitop3_b32 %[a3], %[a3], %[w4], %[w5] bitop3:0x96\n"
+      "v_xor_b32 %[a3], %[a3], %[w6]\n"
+      "v_bitop3_b32 %[a4], %[a4], %[w5], %[w6] bitop3:0x96\n"
+      "v_xor_b32 %[a4], %[a4], %[w7]\n"
+      "v_bitop3_b32 %[a5], %[a5], %[w6], %[w7] bitop3:0x96\n"
+      "v_xor_b32 %[a5], %[a5], %[w8]\n"
+      "v_bitop3_b32 %[a6], %[a6], %[w7], %[w8] bitop3:0x96\n"
+      "v_xor_b32 %[a6], %[a6], %[w9]\n"
+      "v_bitop3_b32 %[a7], %[a7], %[w8], %[w9] bitop3:0x96\n"
+      "v_xor_b32 %[a7], %[a7], %[w10]\n"
+      "v_bitop3_b32 %[a8], %[a8], %[w9], %[w10] bitop3:0x96\n"
+      "v_xor_b32 %[a8], %[a8], %[w11]\n"
+      "v_bitop3_b32 %[a9], %[a9], %[w10], %[w11] bitop3:0x96\n"
+      "v_xor_b32 %[a9], %[a9], %[w12]\n"
+      "s_branch .Lqendx%=\n"
+      ".Lqb0k15x%=:\n"
+      "v_bitop3_b32 %[a0], %[a0], %[w0], %[w1] bitop3:0x96\n"
+      "v_bitop3_b32 %[a0], %[a0], %[w2], %[w3] bitop3:0x96\n"
+      "v_bitop3_b32 %[a1], %[a1], %[w1], %[w2] bitop3:0x96\n"
+      "v_bitop3_b32 %[a1], %[a1], %[w3], %[w4] bitop3:0x96\n"
+      "v_bitop3_b32 %[a2], %[a2], %[w2], %[w3] bitop3:0x96\n"
+      "v_bitop3_b32 %[a2], %[a2], %[w4], %[w5] bitop3:0x96\n"
+      "v_bitop3_b32 %[a3], %[a3], %[w3], %[w4] bitop3:0x96\n"
+      "v_bitop3_b32 %[a3], %[a3], %[w5], %[w6] bitop3:0x96\n"
+      "v_bitop3_b32 %[a4], %[a4], %[w4], %[w5] bitop3:0x96\n"
+      "v_bitop3_b32 %[a4], %[a4], %[w6], %[w7] bitop3:0x96\n"
+      "v_bitop3_b32 %[a5], %[a5], %[w5], %[w6] bitop3:0x96\n"
+      "v_bitop3_b32 %[a5], %[a5], %[w7], %[w8] bitop3:0x96\n"
+      "v_bitop3_b32 %[a6], %[a6], %[w6], %[w7] bitop3:0x96\n"
+      "v_bitop3_b32 %[a6], %[a6], %[w8], %[w9] bitop3:0x96\n"
+      "v_bitop3_b32 %[a7], %[a7], %[w7], %[w8] bitop3:0x96\n"
+      "v_bitop3_b32 %[a7], %[a7], %[w9], %[w10] bitop3:0x96\n"
+      "v_bitop3_b32 %[a8], %[a8], %[w8], %[w9] bitop3:0x96\n"
+      "v_bitop3_b32 %[a8], %[a8], %[w10], %[w11] bitop3:0x96\n"
+      "v_bitop3_b32 %[a9], %[a9], %[w9], %[w10] bitop3:0x96\n"
+      "v_bitop3_b32 %[a9], %[a9], %[w11], %[w12] bitop3:0x96\n"
+      ".Lqendx%=:\n"
+      : [a0] "+v"(acc[0]), [a1] "+v"(acc[1]), [a2] "+v"(acc[2]), [a3] "+v"(acc[3]), [a4] "+v"(acc[4]), [a5] "+v"(acc[5]), [a6] "+v"(acc[6]), [a7] "+v"(acc[7]), [a8] "+v"(acc[8]), [a9] "+v"(acc[9])
+      : [w0] "v"(w[0]), [w1] "v"(w[1]), [w2] "v"(w[2]), [w3] "v"(w[3]), [w4] "v"(w[4]), [w5] "v"(w[5]), [w6] "v"(w[6]), [w7] "v"(w[7]), [w8] "v"(w[8]), [w9] "v"(w[9]), [w10] "v"(w[10]), [w11] "v"(w[11]), [w12] "v"(w[12]), [c] "s"(code)
+      : "scc");
+}
 __device__ __forceinline__ uint4 lds_b64x2(const uint32_t* p) {  // 8-byte aligned: two ds_read_b64
   const uint2 lo = *reinterpret_cast<const uint2*>(p), hi = *reinterpret_cast<const uint2*>(p + 2);
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
@@ -330,6 +602,7 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
             const uint4 nx = lds_b64x2(yw + 4 * q + 16);
             const int rot = (4 * q) & 15;
             const uint32_t word = q < 8 ? lo : hi;
+#if FKS_JUMP_PAIRS  // A/B: two 2-bit steps
 #pragma unroll
             for (int d = 0; d < 4; d += 2) {
               // coefficients 64 wd + 4q + d, +1 as a wave-uniform 2-bit code: a scalar
@@ -342,6 +615,16 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
                                win[(rot + d + 6) & 15], win[(rot + d + 7) & 15], win[(rot + d + 8) & 15],
                                win[(rot + d + 9) & 15], win[(rot + d + 10) & 15], two);
             }
+#else
+            {
+              // coefficients 64 wd + 4q .. +3 as one wave-uniform 4-bit code
+              const uint32_t quad = (word >> ((4 * q) & 31)) & 15u;
+              uint32_t w13[13];
+#pragma unroll
+              for (int t = 0; t < 13; t++) w13[t] = win[(rot + t) & 15];
+              jump_quad_step10(acc, w13, quad);
+            }
+#endif
             win[(rot + 0) & 15] = nx.x;
             win[(rot + 1) & 15] = nx.y;
             win[(rot + 2) & 15] = nx.z;
