@@ -1954,7 +1954,10 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
     };
     // (issuing seed k+1's lookups, z and g z ahead of seed k's p-dependent tail, which
     // removes the wait state between the tail's dependent packed ops, measured 1 % slower:
-    // profiles/r04d_pipe_ab.log)
+    // profiles/r04d_pipe_ab.log; dropping the wd0 tail's fma -- t = gz for wd = +0 and a
+    // finite p, with the chain redone exactly for the lanes that end non-finite -- issues one
+    // packed op per element pair and seed fewer but measured 1.5 % slower, its lr*gz waiting
+    // on gz's conversions: profiles/r04o_wd0_nofma_ab.log)
     {
 #pragma unroll
       for (int k = 0; k < kBsSeeds; k++) {
