@@ -2303,6 +2303,7 @@ __device__ __forceinline__ float phx_cast(float v) {  // static_cast<scalar_t>(f
 // fks_device_selfcheck(FKS_CHECK_PHILOX_RADIUS) compares phx_radius2 with ocml's
 // sqrtf(-2 logf(u)) on all 2^32 words; tests/test_gpu_torch_rocm.py the whole stream with
 // torch.normal on the device.
+template <bool kExact = true>
 __device__ __forceinline__ f32x2_t phx_radius2(const f32x2_t u) {
   const f32x2_t y = {__builtin_amdgcn_logf(u.x), __builtin_amdgcn_logf(u.y)};
   const f32x2_t m2hi = {__uint_as_float(0xbfb17217u), __uint_as_float(0xbfb17217u)};  // -2 x 0x3f317217
@@ -2312,6 +2313,7 @@ __device__ __forceinline__ f32x2_t phx_radius2(const f32x2_t u) {
   e = __builtin_elementwise_fma(m2lo, y, e);
   const f32x2_t x = r + e;
   f32x2_t sq = {__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
+  if (!kExact) return sq;  // within 1 ulp of the correctly rounded root (phx_z_bf16)
   const f32x2_t sm = {__int_as_float(__float_as_int(sq.x) - 1), __int_as_float(__float_as_int(sq.y) - 1)};
   const f32x2_t sp = {__int_as_float(__float_as_int(sq.x) + 1), __int_as_float(__float_as_int(sq.y) + 1)};
   const f32x2_t rm = __builtin_elementwise_fma(-sm, sq, x), rp = __builtin_elementwise_fma(-sp, sq, x);
@@ -2322,10 +2324,11 @@ __device__ __forceinline__ f32x2_t phx_radius2(const f32x2_t u) {
   return sq;
 }
 
+template <bool kExact = true>
 __device__ __forceinline__ void phx_box_muller2(const uint4 w, f32x2_t& zA, f32x2_t& zB) {
   const f32x2_t cu = {2.3283064e-10f, 2.3283064e-10f}, cv = {1.46291807e-09f, 1.46291807e-09f};
   const f32x2_t fx = {(float)w.x, (float)w.z}, fy = {(float)w.y, (float)w.w};
-  const f32x2_t sq = phx_radius2(__builtin_elementwise_fma(fx, cu, cu));
+  const f32x2_t sq = phx_radius2<kExact>(__builtin_elementwise_fma(fx, cu, cu));
   const f32x2_t v = __builtin_elementwise_fma(fy, cv, cv);
   const f32x2_t rev = v * (f32x2_t){__uint_as_float(0x3e22f983u), __uint_as_float(0x3e22f983u)};  // 1/(2 pi)
   const f32x2_t sc1 = {__builtin_amdgcn_sinf(rev.x), __builtin_amdgcn_cosf(rev.x)};
@@ -2333,6 +2336,29 @@ __device__ __forceinline__ void phx_box_muller2(const uint4 w, f32x2_t& zA, f32x
   const f32x2_t zero = {0.0f, 0.0f};
   zA = __builtin_elementwise_fma(sc1, (f32x2_t){sq.x, sq.x}, zero);
   zB = __builtin_elementwise_fma(sc2, (f32x2_t){sq.y, sq.y}, zero);
+}
+
+// The four z of one Philox output rounded to bf16.  Only the bf16 value matters here, so
+// the radius's +-1 ulp correction (a third of phx_radius2's instructions) is skipped
+// unless it could change it: with the root within 1 ulp, z = (sin or cos) s moves by at
+// most 3 f32 ulps, which changes the bf16 rounding only for a product within 3 ulps of a
+// rounding midpoint (low 16 bits 0x8000; across a binade both round to the power of two).
+// Lanes with any of their four products within 4 ulps of one redo the pair exactly (about
+// 3.5 % of the waves' iterations branch).
+__device__ __forceinline__ bool phx_near_bf16_mid(float z) {
+  return ((__float_as_uint(z) & 0xFFFFu) - 0x7FFCu) <= 8u;
+}
+__device__ __forceinline__ void phx_z_bf16(const uint4 w, f32x2_t& zA, f32x2_t& zB) {
+#if FKS_PHX_EXACT_RADIUS  // A/B: the corrected radius always
+  phx_box_muller2<true>(w, zA, zB);
+#else
+  phx_box_muller2<false>(w, zA, zB);
+  const bool near = (int)phx_near_bf16_mid(zA.x) | (int)phx_near_bf16_mid(zA.y) | (int)phx_near_bf16_mid(zB.x) |
+                    (int)phx_near_bf16_mid(zB.y);
+  if (__builtin_expect(near, 0)) phx_box_muller2<true>(w, zA, zB);
+#endif
+  zA = rnd2<FKS_BF16>(zA);
+  zB = rnd2<FKS_BF16>(zB);
 }
 
 // the radius of one word as ocml computes it (the reference's instructions), for the
@@ -2374,9 +2400,13 @@ __device__ __forceinline__ void phx_item(const PhiloxArgs& a, const PhxTensor& T
     const f32x2_t zA = {phx_cast<DT>(b1.x), phx_cast<DT>(b1.y)}, zB = {phx_cast<DT>(b2.x), phx_cast<DT>(b2.y)};
 #else
     f32x2_t zA, zB;
-    phx_box_muller2(w, zA, zB);
-    zA = (f32x2_t){phx_cast<DT>(zA.x), phx_cast<DT>(zA.y)};
-    zB = (f32x2_t){phx_cast<DT>(zB.x), phx_cast<DT>(zB.y)};
+    if constexpr (DT == FKS_BF16) {
+      phx_z_bf16(w, zA, zB);
+    } else {
+      phx_box_muller2(w, zA, zB);
+      zA = (f32x2_t){phx_cast<DT>(zA.x), phx_cast<DT>(zA.y)};
+      zB = (f32x2_t){phx_cast<DT>(zB.x), phx_cast<DT>(zB.y)};
+    }
 #endif
     if (MODE == kModeWriteZ) {
       pA = zA;
