@@ -1761,12 +1761,26 @@ __device__ __forceinline__ uint32_t bs_index(uint32_t w, int c) {
   }
 }
 
+#if FKS_BS_WGTIME  // diagnostic build: per-workgroup start and per-wave end times (100 MHz)
+__device__ uint64_t g_bs_wgtime[4096][16];
+extern "C" int fks_debug_bs_wgtime(uint64_t* out, int nblocks) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bs_wgtime), sizeof(uint64_t) * 16 * (size_t)nblocks, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
+
 template <int MODE, bool FULL>
 __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   if ((uint32_t)(size_t)(lds_u32_t*)lds32 != 0u) __builtin_trap();
   const int tid = threadIdx.x;
   const int lane = tid & 63;
+#if FKS_BS_WGTIME
+  if (tid == 0) g_bs_wgtime[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
+  auto stamp = [&]() { if (lane == 0) g_bs_wgtime[blockIdx.x][1 + (tid >> 6)] = __builtin_amdgcn_s_memrealtime(); };
+#else
+  auto stamp = [&]() {};
+#endif
   const int half = __builtin_amdgcn_readfirstlane(tid >= kBsHalfThreads ? 1 : 0);
   const int ht = tid - half * kBsHalfThreads;
   const int hw = __builtin_amdgcn_readfirstlane(ht >> 6);
@@ -2010,7 +2024,7 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
 
   // two named slots and a loop unrolled by two: a slot copy on the back edge would wait
   // for the load -- and the store before it -- at the top of every task
-  if (hw >= ntask) return;
+  if (hw >= ntask) { stamp(); return; }
   if (ordered && half) await_stored(hw);
   Slot s0 = fetch(hw), s1;
   int n = hw;
@@ -2023,6 +2037,7 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
     n += kBsWaves;
   }
   if (ordered && half == 0) publish_stored(n);  // the wave's last task
+  stamp();
 }
 
 // ------------------------------------------------------------------ irregular kernel
