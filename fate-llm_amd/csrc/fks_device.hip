@@ -223,7 +223,7 @@ __device__ __forceinline__ bool dev_value_apply(const float* v) {
 // y[i + 10l .. i + 10l + 15] in a 16-register sliding window fed by two ds_read_b64
 // per step:  acc[j] ^= y[i + d + 10l + j] & -c[i + d]   (d = 0..3, j = 0..9).
 constexpr int kJumpXOff = 3;            // x at word 3 -> y = x + 1 at word 4 (16 B aligned)
-constexpr int kJumpLdsWords = kJumpXOff + kJumpXLen + 64;  // + over-read slack of the last window
+[[maybe_unused]] constexpr int kJumpLdsWords = kJumpXOff + kJumpXLen + 64;  // + over-read slack of the last window
 
 // acc[j] ^= c0 * w[j] ^ c1 * w[j + 1] (j < 10) for the wave-uniform coefficient pair
 // two = c0 | c1 << 1 (63 lanes x 10 words cover the 624 state words).  Scalar branches
@@ -542,6 +542,121 @@ __device__ __forceinline__ uint4 lds_b64x2(const uint32_t* p) {  // 8-byte align
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
 }
 
+#if !FKS_JUMP_1PHASE
+// The sweep in two phases of 156 coefficient words (9984 coefficients) each, so that LDS
+// holds only the x words one phase's windows read (10,624 words, 42.5 KB, plus the 624
+// seeding words) instead of all 20,561: two workgroups per CU instead of one, 8 waves per
+// SIMD to hide the scalar branches of the 4-bit steps.  The phases take turns in LDS
+// between a wave's jobs (A B, B A, ...): the accumulation is an xor, so their order does
+// not matter, and each switch regenerates the other phase's words from 624 saved ones.
+constexpr int kJumpPhaseWd = 156;                     // coefficient words (of 312) per phase
+constexpr int kJumpPhaseX = 64 * kJumpPhaseWd + 640;  // x words a phase reads: 9984 + 10 x 62 + 19 + 1, rounded up
+constexpr int kJumpInitOff = kJumpXOff + kJumpPhaseX;  // the 624 seeding words, kept for phase A
+constexpr int kJumpLds2Words = kJumpInitOff + kMtN;
+
+__global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_j[];
+  uint32_t* lx = lds_j + kJumpXOff;  // phase P: lx[t] = x[9984 P + t]
+  uint32_t* x0 = lds_j + kJumpInitOff;
+  const int tid = threadIdx.x;
+  const int k = blockIdx.x;
+  const uint64_t seed = a.seeds[k];
+  // mt19937::init_with_uint32 (MT19937RNGEngine.h:156-162): a serial recurrence
+  if (tid == 0) {
+    uint32_t s = (uint32_t)(seed & 0xffffffffu);
+    x0[0] = s;
+    for (int j = 1; j < kMtN; j++) {
+      s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)j;
+      x0[j] = s;
+    }
+  }
+  __syncthreads();
+  // fill LDS with phase P's words: its first 624 (the seeding words, or x[9984..10607]
+  // from phase A's words in place), then x[n] = x[n-227] ^ twist(x[n-624], x[n-623]) in
+  // steps of 227 independent words.  Callers are past a barrier that ends every read of
+  // the other phase.
+  auto fill = [&](const int P) {
+    if (tid < kMtN) lx[tid] = P == 0 ? x0[tid] : lx[64 * kJumpPhaseWd + tid];
+    __syncthreads();
+    for (int base = kMtN; base < kJumpPhaseX; base += kMtN - kMtM) {
+      const int n = base + tid;
+      if (tid < kMtN - kMtM && n < kJumpPhaseX) lx[n] = lx[n - (kMtN - kMtM)] ^ mt_twist(lx[n - kMtN], lx[n - kMtN + 1]);
+      __syncthreads();
+    }
+  };
+  fill(0);
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  constexpr int kW = 10, kLanes = 63;  // 63 lanes x 10 words (lane 62 keeps words 620..623)
+  const uint32_t* yb = lx + 1 + kW * lane;  // y[9984 P + kW lane]
+  const int c0 = blockIdx.y * a.chunks_per_wg;
+  const int c1 = min(c0 + a.chunks_per_wg, a.nchunks);
+  const int st = a.stride > 0 ? a.stride : 1;
+  constexpr int kWaves = kJumpThreads / 64;
+  const int nround = (c1 - c0 + kWaves - 1) / kWaves;  // workgroup-uniform
+  int P = 0;  // the phase in LDS
+  for (int r = 0; r < nround; r++) {
+    const int c = c0 + wave + kWaves * r;
+    const bool job = c < c1 && lane < kLanes;
+    const int64_t b = c < c1 ? a.chunk_block[(size_t)c * st] : 0;
+    const bool sweep = c < c1 && b != 0;  // wave-uniform
+    const uint64_t* poly = a.polys + (size_t)(c < c1 ? c : c0) * st * 312;  // wave-uniform: scalar loads
+    uint32_t acc[kW];
+#pragma unroll
+    for (int j = 0; j < kW; j++) acc[j] = 0u;
+    if (job && b == 0) {
+#pragma unroll
+      for (int j = 0; j < kW; j++) acc[j] = kW * lane + j < kMtN ? x0[kW * lane + j] : 0u;
+    }
+    for (int h = 0; h < 2; h++) {
+      if (h == 1) {  // switch the phase in LDS
+        __syncthreads();
+        P ^= 1;
+        fill(P);
+      }
+      if (sweep && lane < kLanes) {
+        uint32_t win[16];
+        {
+          const uint4 q0 = lds_b64x2(yb), q1 = lds_b64x2(yb + 4), q2 = lds_b64x2(yb + 8), q3 = lds_b64x2(yb + 12);
+          win[0] = q0.x; win[1] = q0.y; win[2] = q0.z; win[3] = q0.w;
+          win[4] = q1.x; win[5] = q1.y; win[6] = q1.z; win[7] = q1.w;
+          win[8] = q2.x; win[9] = q2.y; win[10] = q2.z; win[11] = q2.w;
+          win[12] = q3.x; win[13] = q3.y; win[14] = q3.z; win[15] = q3.w;
+        }
+        const uint64_t* pw = poly + kJumpPhaseWd * P;
+        uint64_t next = pw[0];
+        for (int wd = 0; wd < kJumpPhaseWd; wd++) {
+          const uint64_t bits = next;
+          if (wd + 1 < kJumpPhaseWd) next = pw[wd + 1];  // prefetch the next 64 coefficients
+          const uint32_t lo = (uint32_t)bits, hi = (uint32_t)(bits >> 32);
+          const uint32_t* yw = yb + 64 * wd;
+#pragma unroll
+          for (int q = 0; q < 16; q++) {
+            // window = y[9984 P + 64 wd + 4q + kW lane + 0..15], stored rotated by 4q (mod 16)
+            const uint4 nx = lds_b64x2(yw + 4 * q + 16);
+            const int rot = (4 * q) & 15;
+            const uint32_t word = q < 8 ? lo : hi;
+            const uint32_t quad = (word >> ((4 * q) & 31)) & 15u;
+            uint32_t w13[13];
+#pragma unroll
+            for (int t = 0; t < 13; t++) w13[t] = win[(rot + t) & 15];
+            jump_quad_step10(acc, w13, quad);
+            win[(rot + 0) & 15] = nx.x;
+            win[(rot + 1) & 15] = nx.y;
+            win[(rot + 2) & 15] = nx.z;
+            win[(rot + 3) & 15] = nx.w;
+          }
+        }
+      }
+    }
+    if (job) {
+      uint32_t* out = a.states + ((size_t)(a.use_slot ? a.slot[k] : (uint32_t)k) * a.nchunks + c) * kMtN + kW * lane;
+#pragma unroll
+      for (int j = 0; j < kW; j += 2)
+        if (kW * lane + j < kMtN) *reinterpret_cast<uint2*>(out + j) = make_uint2(acc[j], acc[j + 1]);
+    }
+  }
+}
+#else  // A/B: one phase, all 20,561 x words in LDS (one workgroup per CU)
 __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_j[];
   uint32_t* xs = lds_j + kJumpXOff;
@@ -639,6 +754,7 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
     }
   }
 }
+#endif
 
 // ------------------------------------------------------------------ apply kernel
 // LDS accessors by byte offset.  The apply kernel's only LDS is its dynamic block,
@@ -2554,7 +2670,11 @@ static int ensure_lds_attr(PerDevice& once, K* fn, int bytes) {
 }
 
 int launch_jump(const JumpArgs& a, int nseeds, void* stream) {
+#if FKS_JUMP_1PHASE
   const size_t lds = sizeof(uint32_t) * (size_t)kJumpLdsWords;
+#else
+  const size_t lds = sizeof(uint32_t) * (size_t)kJumpLds2Words;
+#endif
   static PerDevice attr;
   if (int e = ensure_lds_attr(attr, &fks_jump_kernel, (int)lds)) return e;
   dim3 grid((unsigned)nseeds, (unsigned)((a.nchunks + a.chunks_per_wg - 1) / a.chunks_per_wg));
