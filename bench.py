@@ -108,6 +108,18 @@ def pmc_summary_name(wd):
     return PMC_SUMMARIES["wd0" if wd == 0.0 else "wd"]
 
 
+def lds_active_frac(pmc):
+    """LDS-array cycles (bank conflicts included) per CU-cycle of the dominant kernel:
+    rocprofv3 SQ_LDS_IDX_ACTIVE over 256 CUs x GRBM_GUI_ACTIVE / 8 (tools/summarize_pmc2.py);
+    beside valu_active_frac, the slice kernel's other co-limit."""
+    if pmc.get("lds_active_frac") is not None:
+        return round(pmc["lds_active_frac"], 4)
+    c, clk = pmc.get("per_launch") or {}, pmc.get("clock_cycles_per_launch")
+    if c.get("SQ_LDS_IDX_ACTIVE") and clk:
+        return round(c["SQ_LDS_IDX_ACTIVE"] / 256 / clk, 4)
+    return None
+
+
 def load_pmc_summary(wd=None, name=None):
     """Per-launch counters of the dominant kernel from the committed rocprofv3 --pmc
     passes (profiles/PMC_SUMMARIES, written by tools/summarize_pmc2.py)."""
@@ -448,8 +460,9 @@ def run(args, world, rank, local):
                 "avg_launch_ms": round(prof.apply_ms / n_apply, 3),
                 "units_per_launch": units, "lane_ops_per_unit": round(lane_ops, 3),
                 "build_id": build_id,
-                "counters": {k: pmc.get(k) for k in ("valu_active_frac", "valu_dual_issue_frac", "wait_any_frac",
-                                                     "lds_bank_conflict_frac", "clock_ghz")},
+                "counters": dict({k: pmc.get(k) for k in ("valu_active_frac", "valu_dual_issue_frac", "wait_any_frac",
+                                                          "lds_bank_conflict_frac", "clock_ghz")},
+                                 lds_active_frac=lds_active_frac(pmc)),
                 "unit_def": ("one seed*param update (z draw + update chain); lane-ops = rocprofv3 SQ_INSTS_VALU x 64 "
                              f"per seed*param (profiles/{pmc_summary_name(wd)}); peak = 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz "
                              "(MI355X_MICROARCH.md); mix_ceiling = the same chip issuing this kernel's "

@@ -66,6 +66,8 @@ def main(tag, variant, params, seeds, kernel=None, elt=2):
         "wait_any_frac": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"],
         "wait_inst_any_frac": c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"],
         "lds_bank_conflict_frac": (c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"] if c.get("SQ_LDS_IDX_ACTIVE") else None),
+        # LDS-array cycles (conflicts included) per CU-cycle, 256 CUs
+        "lds_active_frac": (c["SQ_LDS_IDX_ACTIVE"] / 256 / clk_cycles if c.get("SQ_LDS_IDX_ACTIVE") else None),
         "clock_cycles_per_launch": clk_cycles,
         # effective clock (MI355X_MICROARCH.md: GRBM_GUI_ACTIVE / 8 / wall time); profiled
         # passes run slightly slower than unprofiled ones
