@@ -2077,6 +2077,8 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
       p.y = ST::cvt(odd ? keep : got);
     }
     auto z_of = [&](const int k) __attribute__((always_inline)) -> f32x2_t {
+      // (R read through the vector-memory path instead, an L1-resident 1 KB table off the
+      // LDS: 13 % slower, profiles/r04rg_r_global_ab.log)
       const float r = lds_f32(bs_index<2>(oa[k & 7], k >> 3));
       const f32x2_t rr = {r, r}, zero = {0.0f, 0.0f};
       const f32x2_t cs = lds_f32x2(1024u + bs_index<3>(ob[k & 7], k >> 3));
@@ -2124,7 +2126,9 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   auto task = [&](const int n, const Slot& sl, Slot& nx) {
     uint32_t oa[8], ob[8];
     __builtin_amdgcn_s_setprio(2);
+#if !FKS_BS_DIAG_NOWAIT  // diagnostic (wrong values): no hand-off wait, the resource bound
     while (__builtin_amdgcn_readfirstlane(bs_flag_load(flag)) < (uint32_t)n) __builtin_amdgcn_s_sleep(0);
+#endif
     asm volatile("" ::: "memory");
     twist(n, oa, ob);
     if (lane == 0) bs_flag_store(flag, (uint32_t)n + 1u);
@@ -2135,7 +2139,11 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
       await_stored(n + kBsWaves);
     }
     nx = fetch(n + kBsWaves);
+#if FKS_BS_DIAG_NOCHAIN  // diagnostic (wrong values): the twist and its hand-offs alone
+    if (__builtin_amdgcn_readfirstlane(oa[0] ^ ob[0]) == 0x12345u) chain(sl, oa, ob);
+#else
     chain(sl, oa, ob);
+#endif
   };
 
   // two named slots and a loop unrolled by two: a slot copy on the back edge would wait
