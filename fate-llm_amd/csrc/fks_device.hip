@@ -216,55 +216,16 @@ __device__ __forceinline__ bool dev_value_apply(const float* v) {
 
 // ------------------------------------------------------------------ jump kernel
 // grid (nseeds, ceil(nchunks / chunks_per_wg)); block kJumpThreads (16 waves).
-// LDS holds the seed's x[0..20560] (+ slack read by the last sliding window) at a
-// 3-word offset, so that y = x + 1 is 16-byte aligned.  Each wave evaluates the jump
+// LDS holds one phase of the seed's x words (below) at a 3-word offset, so that
+// y = x + 1 is 16-byte aligned.  Each wave evaluates the jump
 // of one chunk at a time: lane l < 63 owns window words w = 10l .. 10l+9 and sweeps
-// the 19937 coefficients of c(t) = t^J mod phi four at a time, keeping
+// the 19937 coefficients of c(t) = t^J mod phi four at a time (jump_quad_step10; the
+// 2-bit pair step it replaced and the one-phase kernel are in git history (commit
+// 9dd4861); A/B logs profiles/r04n_jump_quad_ab.log, r04x_jump_2phase_ab.log), keeping
 // y[i + 10l .. i + 10l + 15] in a 16-register sliding window fed by two ds_read_b64
 // per step:  acc[j] ^= y[i + d + 10l + j] & -c[i + d]   (d = 0..3, j = 0..9).
 constexpr int kJumpXOff = 3;            // x at word 3 -> y = x + 1 at word 4 (16 B aligned)
-[[maybe_unused]] constexpr int kJumpLdsWords = kJumpXOff + kJumpXLen + 64;  // + over-read slack of the last window
 
-// acc[j] ^= c0 * w[j] ^ c1 * w[j + 1] (j < 10) for the wave-uniform coefficient pair
-// two = c0 | c1 << 1 (63 lanes x 10 words cover the 624 state words).  Scalar branches
-// skip a clear pair and pick the one-word or the 3-input-xor body (v_bitop3), so a
-// random polynomial costs 0.75 VALU ops per word and coefficient pair instead of 2.
-// Inline asm: compiled from C the three bodies write fresh registers and every merge
-// copies the accumulators back.
-__device__ __forceinline__ void jump_pair_step10(uint32_t (&acc)[10], uint32_t w0, uint32_t w1, uint32_t w2,
-                                                 uint32_t w3, uint32_t w4, uint32_t w5, uint32_t w6, uint32_t w7,
-                                                 uint32_t w8, uint32_t w9, uint32_t w10, uint32_t two) {
-  asm volatile(
-      "s_cmp_eq_u32 %[two], 0\n\t"
-      "s_cbranch_scc1 .Lkend%=\n\t"
-      "s_cmp_eq_u32 %[two], 3\n\t"
-      "s_cbranch_scc1 .Lkboth%=\n\t"
-      "s_cmp_eq_u32 %[two], 1\n\t"
-      "s_cbranch_scc1 .Lkone%=\n\t"
-      "v_xor_b32 %0, %0, %[w1]\n\tv_xor_b32 %1, %1, %[w2]\n\tv_xor_b32 %2, %2, %[w3]\n\t"
-      "v_xor_b32 %3, %3, %[w4]\n\tv_xor_b32 %4, %4, %[w5]\n\tv_xor_b32 %5, %5, %[w6]\n\t"
-      "v_xor_b32 %6, %6, %[w7]\n\tv_xor_b32 %7, %7, %[w8]\n\tv_xor_b32 %8, %8, %[w9]\n\t"
-      "v_xor_b32 %9, %9, %[w10]\n\t"
-      "s_branch .Lkend%=\n"
-      ".Lkone%=:\n\t"
-      "v_xor_b32 %0, %0, %[w0]\n\tv_xor_b32 %1, %1, %[w1]\n\tv_xor_b32 %2, %2, %[w2]\n\t"
-      "v_xor_b32 %3, %3, %[w3]\n\tv_xor_b32 %4, %4, %[w4]\n\tv_xor_b32 %5, %5, %[w5]\n\t"
-      "v_xor_b32 %6, %6, %[w6]\n\tv_xor_b32 %7, %7, %[w7]\n\tv_xor_b32 %8, %8, %[w8]\n\t"
-      "v_xor_b32 %9, %9, %[w9]\n\t"
-      "s_branch .Lkend%=\n"
-      ".Lkboth%=:\n\t"
-      "v_bitop3_b32 %0, %0, %[w0], %[w1] bitop3:0x96\n\tv_bitop3_b32 %1, %1, %[w1], %[w2] bitop3:0x96\n\t"
-      "v_bitop3_b32 %2, %2, %[w2], %[w3] bitop3:0x96\n\tv_bitop3_b32 %3, %3, %[w3], %[w4] bitop3:0x96\n\t"
-      "v_bitop3_b32 %4, %4, %[w4], %[w5] bitop3:0x96\n\tv_bitop3_b32 %5, %5, %[w5], %[w6] bitop3:0x96\n\t"
-      "v_bitop3_b32 %6, %6, %[w6], %[w7] bitop3:0x96\n\tv_bitop3_b32 %7, %7, %[w7], %[w8] bitop3:0x96\n\t"
-      "v_bitop3_b32 %8, %8, %[w8], %[w9] bitop3:0x96\n\tv_bitop3_b32 %9, %9, %[w9], %[w10] bitop3:0x96\n"
-      ".Lkend%=:"
-      : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]),
-        "+v"(acc[7]), "+v"(acc[8]), "+v"(acc[9])
-      : [w0] "v"(w0), [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4), [w5] "v"(w5), [w6] "v"(w6),
-        [w7] "v"(w7), [w8] "v"(w8), [w9] "v"(w9), [w10] "v"(w10), [two] "s"(two)
-      : "scc");
-}
 // acc[j] ^= XOR over the set bits d of the wave-uniform 4-bit code of w[d + j] (j < 10):
 // coefficients 4 at a time.  A binary tree of scalar bit tests picks one of 16 bodies
 // (none, one v_xor_b32, one v_bitop3_b32, or two of them per word), so a random polynomial
@@ -542,7 +503,6 @@ __device__ __forceinline__ uint4 lds_b64x2(const uint32_t* p) {  // 8-byte align
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
 }
 
-#if !FKS_JUMP_1PHASE
 // The sweep in two phases of 156 coefficient words (9984 coefficients) each, so that LDS
 // holds only the x words one phase's windows read (10,624 words, 42.5 KB, plus the 624
 // seeding words) instead of all 20,561: two workgroups per CU instead of one, 8 waves per
@@ -656,105 +616,6 @@ __global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
     }
   }
 }
-#else  // A/B: one phase, all 20,561 x words in LDS (one workgroup per CU)
-__global__ __launch_bounds__(kJumpThreads) void fks_jump_kernel(JumpArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds_j[];
-  uint32_t* xs = lds_j + kJumpXOff;
-  const int tid = threadIdx.x;
-  const int k = blockIdx.x;
-  const uint64_t seed = a.seeds[k];
-  // mt19937::init_with_uint32 (MT19937RNGEngine.h:156-162): a serial recurrence
-  if (tid == 0) {
-    uint32_t s = (uint32_t)(seed & 0xffffffffu);
-    xs[0] = s;
-    for (int j = 1; j < kMtN; j++) {
-      s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)j;
-      xs[j] = s;
-    }
-  }
-  for (int j = kJumpXLen + tid; j < kJumpLdsWords - kJumpXOff; j += kJumpThreads) xs[j] = 0u;
-  __syncthreads();
-  // x[n] = x[n-227] ^ twist(x[n-624], x[n-623]): 227 independent words per step
-  for (int base = kMtN; base < kJumpXLen; base += kMtN - kMtM) {
-    const int n = base + tid;
-    if (tid < kMtN - kMtM && n < kJumpXLen) xs[n] = xs[n - (kMtN - kMtM)] ^ mt_twist(xs[n - kMtN], xs[n - kMtN + 1]);
-    __syncthreads();
-  }
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  constexpr int kW = 10, kLanes = 63;  // 63 lanes x 10 words (lane 62 keeps words 620..623)
-  const uint32_t* yb = xs + 1 + kW * lane;  // y[kW lane]
-  const int c0 = blockIdx.y * a.chunks_per_wg;
-  const int c1 = min(c0 + a.chunks_per_wg, a.nchunks);
-  for (int c = c0 + wave; c < c1; c += kJumpThreads / 64) {
-    const int st = a.stride > 0 ? a.stride : 1;
-    const int64_t b = a.chunk_block[(size_t)c * st];
-    uint32_t acc[kW];
-#pragma unroll
-    for (int j = 0; j < kW; j++) acc[j] = 0u;
-    if (lane < kLanes) {
-      if (b == 0) {
-#pragma unroll
-        for (int j = 0; j < kW; j++) acc[j] = kW * lane + j < kMtN ? xs[kW * lane + j] : 0u;
-      } else {
-        const uint64_t* poly = a.polys + (size_t)c * st * 312;  // wave-uniform: scalar loads
-        uint32_t win[16];
-        {
-          const uint4 q0 = lds_b64x2(yb), q1 = lds_b64x2(yb + 4), q2 = lds_b64x2(yb + 8), q3 = lds_b64x2(yb + 12);
-          win[0] = q0.x; win[1] = q0.y; win[2] = q0.z; win[3] = q0.w;
-          win[4] = q1.x; win[5] = q1.y; win[6] = q1.z; win[7] = q1.w;
-          win[8] = q2.x; win[9] = q2.y; win[10] = q2.z; win[11] = q2.w;
-          win[12] = q3.x; win[13] = q3.y; win[14] = q3.z; win[15] = q3.w;
-        }
-        uint64_t next = poly[0];
-        for (int wd = 0; wd < 312; wd++) {
-          const uint64_t bits = next;
-          if (wd + 1 < 312) next = poly[wd + 1];  // prefetch the next 64 coefficients
-          const uint32_t lo = (uint32_t)bits, hi = (uint32_t)(bits >> 32);
-          const uint32_t* yw = yb + 64 * wd;
-#pragma unroll
-          for (int q = 0; q < 16; q++) {
-            // window = y[64 wd + 4q + kW lane + 0..15], stored rotated by 4q (mod 16)
-            const uint4 nx = lds_b64x2(yw + 4 * q + 16);
-            const int rot = (4 * q) & 15;
-            const uint32_t word = q < 8 ? lo : hi;
-#if FKS_JUMP_PAIRS  // A/B: two 2-bit steps
-#pragma unroll
-            for (int d = 0; d < 4; d += 2) {
-              // coefficients 64 wd + 4q + d, +1 as a wave-uniform 2-bit code: a scalar
-              // branch skips clear coefficients, and a set pair costs ONE 3-input xor
-              // per word (v_bitop3), so a random polynomial costs 0.75 instead of 2
-              // VALU ops per word and coefficient pair
-              const uint32_t two = (word >> ((4 * q + d) & 31)) & 3u;
-              jump_pair_step10(acc, win[(rot + d) & 15], win[(rot + d + 1) & 15], win[(rot + d + 2) & 15],
-                               win[(rot + d + 3) & 15], win[(rot + d + 4) & 15], win[(rot + d + 5) & 15],
-                               win[(rot + d + 6) & 15], win[(rot + d + 7) & 15], win[(rot + d + 8) & 15],
-                               win[(rot + d + 9) & 15], win[(rot + d + 10) & 15], two);
-            }
-#else
-            {
-              // coefficients 64 wd + 4q .. +3 as one wave-uniform 4-bit code
-              const uint32_t quad = (word >> ((4 * q) & 31)) & 15u;
-              uint32_t w13[13];
-#pragma unroll
-              for (int t = 0; t < 13; t++) w13[t] = win[(rot + t) & 15];
-              jump_quad_step10(acc, w13, quad);
-            }
-#endif
-            win[(rot + 0) & 15] = nx.x;
-            win[(rot + 1) & 15] = nx.y;
-            win[(rot + 2) & 15] = nx.z;
-            win[(rot + 3) & 15] = nx.w;
-          }
-        }
-      }
-      uint32_t* out = a.states + ((size_t)(a.use_slot ? a.slot[k] : (uint32_t)k) * a.nchunks + c) * kMtN + kW * lane;
-#pragma unroll
-      for (int j = 0; j < kW; j += 2)
-        if (kW * lane + j < kMtN) *reinterpret_cast<uint2*>(out + j) = make_uint2(acc[j], acc[j + 1]);
-    }
-  }
-}
-#endif
 
 // ------------------------------------------------------------------ apply kernel
 // LDS accessors by byte offset.  The apply kernel's only LDS is its dynamic block,
@@ -2678,11 +2539,7 @@ static int ensure_lds_attr(PerDevice& once, K* fn, int bytes) {
 }
 
 int launch_jump(const JumpArgs& a, int nseeds, void* stream) {
-#if FKS_JUMP_1PHASE
-  const size_t lds = sizeof(uint32_t) * (size_t)kJumpLdsWords;
-#else
   const size_t lds = sizeof(uint32_t) * (size_t)kJumpLds2Words;
-#endif
   static PerDevice attr;
   if (int e = ensure_lds_attr(attr, &fks_jump_kernel, (int)lds)) return e;
   dim3 grid((unsigned)nseeds, (unsigned)((a.nchunks + a.chunks_per_wg - 1) / a.chunks_per_wg));
