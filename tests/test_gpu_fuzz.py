@@ -1,0 +1,76 @@
+"""Randomised parity of the drop-in against the CPU oracle: 48 seeded random calls, each a
+random tensor list (1..10 tensors; numel from the serial path's < 16 through ragged sizes
+to 2^17, with every dtype, mixed in one call), random per-tensor lr / weight decay (None,
++0.0, -0.0, 0.01, 0.3), K in 1..80 (the small-K kernel, the 19-seed fp32 and the 32/64-seed
+bf16 slice passes with their remainders), seeds past 2^32, scalars with zeros and edge
+values, applied whole or as 2 or 3 element shards, with the reconstruct window cache on
+or off.  Bit-exact (NaN matches NaN) against oracle.fks_oracle.reconstruct of the whole."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_bitwise
+from oracle import fks_oracle as O
+from test_gpu_parity import DTC, TD, _dev, from_np, to_np
+
+pytestmark = pytest.mark.gpu
+DTYPES = ["float32", "bfloat16", "float16"]
+
+
+def _config(rng):
+    nt = int(rng.integers(1, 11))
+    sizes = []
+    for _ in range(nt):
+        kind = rng.integers(0, 4)
+        if kind == 0:
+            sizes.append(int(rng.integers(1, 16)))                # serial path
+        elif kind == 1:
+            sizes.append(int(rng.integers(16, 2000)))             # ragged
+        elif kind == 2:
+            sizes.append(16 * int(rng.integers(1, 4096)))         # whole 16-blocks
+        else:
+            sizes.append(int(rng.integers(2000, 1 << 17)))
+    dtypes = [DTYPES[int(rng.integers(0, 3))] for _ in range(nt)]
+    if rng.random() < 0.5:  # the common case: one dtype
+        dtypes = [dtypes[0]] * nt
+    lrs = [float(rng.choice([1e-5, 1e-3, 0.5])) for _ in range(nt)]
+    wds = [[None, 0.0, -0.0, 0.01, 0.3][int(rng.integers(0, 5))] for _ in range(nt)]
+    k = int(rng.choice([1, 2, 3, int(rng.integers(4, 20)), 19, 23, 32, 33, 40, 64, int(rng.integers(65, 81))]))
+    seeds = [int(s) for s in rng.integers(0, 2**40, k)]
+    vals = (rng.normal(0.0, 20.0, k)).tolist()
+    for i in range(k):
+        r = rng.random()
+        if r < 0.05:
+            vals[i] = 0.0
+        elif r < 0.08:
+            vals[i] = float(rng.choice([1e-40, -3e38, 1e30, -0.0]))
+    nshards = int(rng.choice([1, 1, 2, 3]))
+    jwin = bool(rng.random() < 0.5)
+    return sizes, dtypes, lrs, wds, seeds, vals, nshards, jwin
+
+
+@pytest.mark.parametrize("case", range(48))
+def test_random_call_matches_oracle(case):
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    rng = np.random.default_rng(1000 + case)
+    sizes, dtypes, lrs, wds, seeds, vals, nshards, jwin = _config(rng)
+    g = torch.Generator().manual_seed(case)
+    base = [to_np((torch.randn(n, generator=g) * 0.02).to(TD[d])) for n, d in zip(sizes, dtypes)]
+    ts = [from_np(a, d, dev) for a, d in zip(base, dtypes)]
+    specs = [codec.ParamSpec(t, lr=lr, weight_decay=wd) for t, lr, wd in zip(ts, lrs, wds)]
+    # train_once drops g == 0.0 entries (fedkseed.py:137; zo_utils.reconstruct_), the oracle too
+    ks = [s for s, v in zip(seeds, vals) if v != 0.0]
+    kv = [v for v in vals if v != 0.0]
+    if ks:
+        if nshards == 1:
+            codec.directional_step(specs, ks, kv, cache_windows=jwin)
+        else:
+            for r in range(nshards):
+                codec.directional_step(specs, ks, kv, shard=r, nshards=nshards, cache_windows=jwin)
+    torch.cuda.synchronize()
+    ref = [a.copy() for a in base]
+    O.reconstruct(ref, [DTC[d] for d in dtypes], lrs, wds, seeds, vals)
+    what = f"case {case}: sizes {sizes} dtypes {dtypes} wds {wds} k {len(seeds)} shards {nshards} jwin {jwin}"
+    for t, r_, d in zip(ts, ref, dtypes):
+        assert_bitwise(to_np(t), r_, d, what)
