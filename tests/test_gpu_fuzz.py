@@ -5,8 +5,6 @@ to 2^17, with every dtype, mixed in one call), random per-tensor lr / weight dec
 bf16 slice passes with their remainders), seeds past 2^32, scalars with zeros and edge
 values, applied whole or as 2 or 3 element shards, with the reconstruct window cache on
 or off.  Bit-exact (NaN matches NaN) against oracle.fks_oracle.reconstruct of the whole."""
-import os
-
 import numpy as np
 import pytest
 import torch
@@ -51,7 +49,6 @@ def _config(rng):
     return sizes, dtypes, lrs, wds, seeds, vals, nshards, jwin
 
 
-@pytest.mark.skipif(not os.environ.get("FKS_FUZZ"), reason="randomised sweep: FKS_FUZZ=1 (not yet run on a GPU box)")
 @pytest.mark.parametrize("case", range(48))
 def test_random_call_matches_oracle(case):
     from fate_llm.algo.fedkseed import codec
