@@ -5,6 +5,8 @@ to 2^17, with every dtype, mixed in one call), random per-tensor lr / weight dec
 bf16 slice passes with their remainders), seeds past 2^32, scalars with zeros and edge
 values, applied whole or as 2 or 3 element shards, with the reconstruct window cache on
 or off.  Bit-exact (NaN matches NaN) against oracle.fks_oracle.reconstruct of the whole."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -74,3 +76,47 @@ def test_random_call_matches_oracle(case):
     what = f"case {case}: sizes {sizes} dtypes {dtypes} wds {wds} k {len(seeds)} shards {nshards} jwin {jwin}"
     for t, r_, d in zip(ts, ref, dtypes):
         assert_bitwise(to_np(t), r_, d, what)
+
+
+def _rocm_reference(params, seeds, vals, lrs, wds):
+    """zo_utils.directional_derivative_step's torch calls on the device (zo_utils.py:42-52),
+    per-tensor lr / wd as the codec's ParamSpecs carry them."""
+    for sd, g in zip(seeds, vals):
+        torch.manual_seed(sd)
+        for p, lr, wd in zip(params, lrs, wds):
+            z = torch.normal(mean=0, std=1, size=p.data.size(), device=p.data.device, dtype=p.data.dtype)
+            if wd is not None:
+                p.data = p.data - lr * (g * z + wd * p.data)
+            else:
+                p.data = p.data - lr * (g * z)
+
+
+@pytest.mark.skipif(not os.environ.get("FKS_FUZZ"), reason="randomised sweep: FKS_FUZZ=1 (not yet run on a GPU box)")
+@pytest.mark.parametrize("case", range(24))
+def test_random_call_matches_torch_on_device(case):
+    """The torch_rocm stream (the reference's z when its model is on the MI355X) on random
+    layouts -- bf16 mostly, where the radius shortcut of phx_z_bf16 applies -- against
+    torch.normal(device="cuda") and the reference's update as torch ops."""
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    rng = np.random.default_rng(5000 + case)
+    nt = int(rng.integers(1, 8))
+    sizes = [int(rng.choice([int(rng.integers(1, 64)), int(rng.integers(64, 5000)), int(rng.integers(5000, 1 << 20))]))
+             for _ in range(nt)]
+    dtypes = [str(rng.choice(["bfloat16", "bfloat16", "bfloat16", "float32", "float16"])) for _ in range(nt)]
+    lrs = [float(rng.choice([1e-5, 1e-3])) for _ in range(nt)]
+    wds = [[None, 0.0, 0.01][int(rng.integers(0, 3))] for _ in range(nt)]
+    k = int(rng.integers(1, 9))
+    seeds = [int(s) for s in rng.integers(0, 2**40, k)]
+    vals = [float(v) for v in rng.normal(0.0, 20.0, k)]
+    g = torch.Generator(dev).manual_seed(case)
+    base = [torch.empty(n, dtype=TD[d], device=dev).normal_(0.0, 0.02, generator=g) for n, d in zip(sizes, dtypes)]
+    got = [b.clone() for b in base]
+    specs = [codec.ParamSpec(t, lr=lr, weight_decay=wd) for t, lr, wd in zip(got, lrs, wds)]
+    codec.directional_step(specs, seeds, vals, stream_mode="torch_rocm")
+    ref = [torch.nn.Parameter(b.clone(), requires_grad=False) for b in base]
+    _rocm_reference(ref, seeds, vals, lrs, wds)
+    torch.cuda.synchronize()
+    what = f"case {case}: sizes {sizes} dtypes {dtypes} wds {wds} k {k}"
+    for a, r, d in zip(got, ref, dtypes):
+        assert_bitwise(to_np(a), to_np(r.data), d, what)
