@@ -5,8 +5,6 @@ to 2^17, with every dtype, mixed in one call), random per-tensor lr / weight dec
 bf16 slice passes with their remainders), seeds past 2^32, scalars with zeros and edge
 values, applied whole or as 2 or 3 element shards, with the reconstruct window cache on
 or off.  Bit-exact (NaN matches NaN) against oracle.fks_oracle.reconstruct of the whole."""
-import os
-
 import numpy as np
 import pytest
 import torch
@@ -91,7 +89,6 @@ def _rocm_reference(params, seeds, vals, lrs, wds):
                 p.data = p.data - lr * (g * z)
 
 
-@pytest.mark.skipif(not os.environ.get("FKS_FUZZ"), reason="randomised sweep: FKS_FUZZ=1 (not yet run on a GPU box)")
 @pytest.mark.parametrize("case", range(24))
 def test_random_call_matches_torch_on_device(case):
     """The torch_rocm stream (the reference's z when its model is on the MI355X) on random
