@@ -17,6 +17,16 @@ pytestmark = pytest.mark.gpu
 DTYPES = ["float32", "bfloat16", "float16"]
 
 
+@pytest.fixture(scope="module", autouse=True)
+def _release_window_cache():
+    """The sweep attaches reconstruct window caches (cache_windows=True); the tests after
+    this module start from none, as they would without it."""
+    yield
+    if torch.cuda.is_available():
+        from fate_llm.algo.fedkseed import codec
+        codec.jwin_release()
+
+
 def _config(rng):
     nt = int(rng.integers(1, 11))
     sizes = []
