@@ -358,6 +358,10 @@ def run(args, world, rank, local):
 
     from fate_llm.algo.fedkseed import codec, zo_utils
 
+    # the headline draws torch's CPU-generator stream (the oracle-pinned one: a reference
+    # client training on the CPU, the tutorial's configuration); the drop-in's default
+    # "auto" would draw the torch_rocm stream on a GPU, which alt_stream times beside it
+    codec.set_stream_mode("torch_cpu")
     dtype = torch.bfloat16
     shapes = [(args.params,)] if args.params else llama7b_shapes()
     total = sum(numel(s) for s in shapes)
@@ -503,7 +507,7 @@ def run(args, world, rank, local):
                     "reconstruct, no collective)") if weak else
                    f"{world}xMI355X: 7B-param bf16 buffer, K=4096 seeds, element-sharded (bit-exact, no collective)",
                    "params": total, "k": args.k, "k_nonzero": len(ks), "tensors": len(shapes),
-                   "lr": 1e-5, "weight_decay": wd,
+                   "lr": 1e-5, "weight_decay": wd, "stream": "torch_cpu",
                    "parallelism": (f"seed-shard{world}" if seed_shard else
                                    f"client-per-gpu{world}" if weak else f"element-shard{world}")},
         "roofline": valu if valu else hbm,

@@ -19,8 +19,15 @@ The z stream (``stream_mode``) is the one the reference draws where its paramete
 * ``"torch_rocm"``: torch's HIP-device generator, Philox4x32-10 + rocrand's Box-Muller in
   torch's grid-stride mapping -- a reference client whose model sits on an MI355X.
 
-All parties of one federation must draw the same stream; the
-default comes from ``FKS_STREAM_MODE`` and ``set_stream_mode``.  Updates are applied in
+All parties of one federation must draw the same stream.  The
+process-wide setting comes from ``FKS_STREAM_MODE`` and ``set_stream_mode``: one of the
+two streams, or ``"auto"`` -- the DEFAULT when ``FKS_STREAM_MODE`` is unset -- which draws
+what the reference draws for the call's tensors: ``torch_rocm`` for tensors on a HIP
+device (every tensor the codec accepts), so a drop-in client on an MI355X gives the bits
+an unmodified reference client on the same device gives.  ``torch_cpu`` (1.8x faster
+here) is the explicit choice for a federation whose reference clients train on the CPU,
+or whose parties are all drop-in clients; the round payloads carry the stream so that a
+drop-in arbiter rejects a mixed federation (payload.py).  Updates are applied in
 place (the reference rebinds ``param.data`` to a new tensor of identical values).
 
 There is no CPU path: tensors must live on a HIP device and libfks.so must be
@@ -42,27 +49,37 @@ from . import _native as N
 
 _DTYPES = {torch.float32: N.F32, torch.bfloat16: N.BF16, torch.float16: N.F16}
 STREAM_MODES = ("torch_cpu", "torch_rocm")
-_stream_mode = os.environ.get("FKS_STREAM_MODE", "torch_cpu")
-if _stream_mode not in STREAM_MODES:
-    raise ValueError(f"FKS_STREAM_MODE must be one of {STREAM_MODES}, not {_stream_mode!r}")
+STREAM_SETTINGS = STREAM_MODES + ("auto",)
+_stream_mode = os.environ.get("FKS_STREAM_MODE") or "auto"
+if _stream_mode not in STREAM_SETTINGS:
+    raise ValueError(f"FKS_STREAM_MODE must be one of {STREAM_SETTINGS}, not {_stream_mode!r}")
 
 
 def set_stream_mode(mode: str) -> None:
-    """The z stream every codec call draws unless told otherwise (module docstring)."""
+    """The z stream every codec call draws unless told otherwise (module docstring):
+    "torch_cpu", "torch_rocm" or "auto" (the stream of the tensors' device)."""
     global _stream_mode
-    if mode not in STREAM_MODES:
-        raise ValueError(f"stream_mode must be one of {STREAM_MODES}, not {mode!r}")
+    if mode not in STREAM_SETTINGS:
+        raise ValueError(f"stream_mode must be one of {STREAM_SETTINGS}, not {mode!r}")
     _stream_mode = mode
 
 
 def get_stream_mode() -> str:
+    """The process-wide setting (possibly "auto"); resolve_stream_mode gives the stream."""
     return _stream_mode
 
 
-def _mode(stream_mode) -> str:
+def resolve_stream_mode(device=None, stream_mode=None) -> str:
+    """The stream a call on tensors of ``device`` draws: ``stream_mode`` if given, else the
+    process-wide setting; "auto" is the stream the reference draws on that device
+    (zo_utils.py:47, optimizer.py:170-172 draw on ``param.data.device``): torch's HIP
+    generator on a HIP device, the CPU generator otherwise (and for ``device=None``, a
+    call with no tensors, which draws nothing)."""
     m = _stream_mode if stream_mode is None else stream_mode
-    if m not in STREAM_MODES:
-        raise ValueError(f"stream_mode must be one of {STREAM_MODES}, not {m!r}")
+    if m not in STREAM_SETTINGS:
+        raise ValueError(f"stream_mode must be one of {STREAM_SETTINGS}, not {m!r}")
+    if m == "auto":
+        return "torch_rocm" if device is not None and torch.device(device).type == "cuda" else "torch_cpu"
     return m
 
 
@@ -85,12 +102,9 @@ class _Batch:
 
     def __init__(self, specs: Sequence[ParamSpec], stream_mode=None):
         self.specs = list(specs)
-        self.stream_mode = _mode(stream_mode)
-        stream_flag = N.STREAM_ROCM if self.stream_mode == "torch_rocm" else 0
         self.copies = []  # (original, contiguous staging) pairs to write back
         self.device = None
-        arr = (N.FksTensor * max(1, len(self.specs)))()
-        for i, sp in enumerate(self.specs):
+        for sp in self.specs:
             t = sp.tensor
             if t.dtype not in _DTYPES:
                 raise NotImplementedError(f"FedKSeed codec: dtype {t.dtype} is not supported on the MI355X path")
@@ -101,6 +115,11 @@ class _Batch:
                 self.device = t.device
             elif t.device != self.device:
                 raise ValueError("FedKSeed codec: all parameters must be on one device")
+        self.stream_mode = resolve_stream_mode(self.device, stream_mode)
+        stream_flag = N.STREAM_ROCM if self.stream_mode == "torch_rocm" else 0
+        arr = (N.FksTensor * max(1, len(self.specs)))()
+        for i, sp in enumerate(self.specs):
+            t = sp.tensor
             if not t.is_contiguous():
                 c = t.contiguous()
                 self.copies.append((t, c))
@@ -399,18 +418,22 @@ def _check_delta(b: _Batch, delta: torch.Tensor) -> None:
 
 
 def delta_accumulate(specs: Sequence[ParamSpec], seeds: Sequence[int], coefs: Sequence[float],
-                     delta: torch.Tensor) -> None:
+                     delta: torch.Tensor, stream_mode=None) -> None:
     """Seed-sharded variant (include/fks.h): delta += f32(coef_s) * z_s for every seed in
-    order, z_s the reference's stream for the spec list (frozen specs draw, are not
-    accumulated); delta is the f32 concatenation of the specs' elements."""
+    order, z_s the reference's CPU stream for the spec list (frozen specs draw, are not
+    accumulated); delta is the f32 concatenation of the specs' elements.  The variant
+    draws the torch_cpu stream only: a call that resolves to torch_rocm raises."""
     if len(seeds) != len(coefs):
         raise ValueError("seeds and coefs differ in length")
     specs = list(specs)
     if not specs or not len(seeds):
         return
-    b = _Batch(specs)
+    b = _Batch(specs, stream_mode)
     if b.device is None:
         return
+    if b.stream_mode != "torch_cpu":
+        raise NotImplementedError("the seed-sharded variant draws the torch_cpu stream only "
+                                  "(stream_mode='torch_cpu' or FKS_STREAM_MODE=torch_cpu)")
     _check_delta(b, delta)
     L = N.load()
     s = np.ascontiguousarray([_seed_u64(x) for x in seeds], dtype=np.uint64)
@@ -428,7 +451,7 @@ def delta_apply(specs: Sequence[ParamSpec], delta: torch.Tensor, decays: Sequenc
         return
     if len(decays) != len(specs):
         raise ValueError("one decay per spec")
-    b = _Batch(specs)
+    b = _Batch(specs, "torch_cpu")  # draws nothing: the stream flag is irrelevant
     if b.device is None:
         return
     _check_delta(b, delta)
@@ -456,7 +479,7 @@ def shard_range(specs: Sequence[ParamSpec], shard: int, nshards: int, stream_mod
 
 def stream_length(tensors: Sequence[torch.Tensor]) -> int:
     """32-bit MT19937 words the tensors consume per seed (their z-stream length)."""
-    b = _Batch([ParamSpec(t) for t in tensors])
+    b = _Batch([ParamSpec(t) for t in tensors], "torch_cpu")
     out = ctypes.c_int64(0)
     N.check(N.load().fks_stream_length(ctypes.addressof(b.arr), b.n, ctypes.byref(out)))
     return int(out.value)

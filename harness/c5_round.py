@@ -42,6 +42,7 @@ import argparse
 import json
 import pickle
 import os
+os.environ.setdefault("FKS_STREAM_MODE", "torch_cpu")  # the CPU-generator stream these measurements use
 import socket
 import sys
 import time

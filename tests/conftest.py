@@ -11,6 +11,10 @@ PKG_PY = os.path.join(ROOT, "fate-llm_amd", "python")
 for p in (ROOT, PKG_PY):
     if p not in sys.path:
         sys.path.insert(0, p)
+# The parity tests compare with the oracle, which restates torch's CPU-generator stream;
+# the drop-in's default ("auto": torch_rocm on a HIP device) is pinned by its own tests
+# (test_stream_tag.py, test_gpu_torch_rocm.py).  Subprocesses inherit this.
+os.environ.setdefault("FKS_STREAM_MODE", "torch_cpu")
 
 
 def pytest_configure(config):

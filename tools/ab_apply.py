@@ -5,6 +5,7 @@ wd AB_WD (default 0.01, 'none' for None) -- and prints the average apply/jump la
 launch for the per-seed figure: 19, or 32 for the bf16 slice kernel)."""
 import json
 import os
+os.environ.setdefault("FKS_STREAM_MODE", "torch_cpu")  # the CPU-generator stream these measurements use
 import subprocess
 import sys
 

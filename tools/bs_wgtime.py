@@ -9,10 +9,11 @@ import argparse
 import ctypes
 import json
 import os
+os.environ.setdefault("FKS_STREAM_MODE", "torch_cpu")  # the CPU-generator stream these measurements use
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "fate-llm_amd", "build", "libfks_wgtime.so")
+LIB = os.path.join(ROOT, "fate-llm_amd", "ab", "libfks_wgtime.so")
 os.environ["FKS_LIB_OVERRIDE"] = LIB
 sys.path.insert(0, os.path.join(ROOT, "fate-llm_amd", "python"))
 sys.path.insert(0, ROOT)

@@ -19,6 +19,7 @@ the two agree bit for bit (tests/test_gpu_c4.py holds the oracle comparison).
 import argparse
 import json
 import os
+os.environ.setdefault("FKS_STREAM_MODE", "torch_cpu")  # the CPU-generator stream these measurements use
 import sys
 import time
 

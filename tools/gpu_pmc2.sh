@@ -14,7 +14,7 @@ GROUPS_=("SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTI
 for v in ${VARIANTS:-full}; do
   # full: the in-tree library at wd 0.01; wd0: the in-tree library at wd 0.0 (kModeUpdateWd0)
   if [ "$v" = "wd0" ]; then unset FKS_LIB_OVERRIDE; export PERF_WD=0.0
-  elif [ "$v" != "full" ]; then export FKS_LIB_OVERRIDE=$PWD/fate-llm_amd/build/libfks_$v.so; unset PERF_WD
+  elif [ "$v" != "full" ]; then export FKS_LIB_OVERRIDE=$PWD/fate-llm_amd/ab/libfks_$v.so; unset PERF_WD
   else unset FKS_LIB_OVERRIDE; unset PERF_WD; fi
   # the device-code identity of the library these passes profile (summarize_pmc2.py records it)
   python3 -c 'import sys; sys.path.insert(0, "fate-llm_amd/python"); from fate_llm.algo.fedkseed import _native; print(_native.build_id())' \

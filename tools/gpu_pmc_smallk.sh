@@ -9,7 +9,7 @@ GROUPS_=("SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTI
          "FETCH_SIZE GRBM_GUI_ACTIVE"
          "WRITE_SIZE GRBM_GUI_ACTIVE")
 for v in ${@:-full}; do
-  if [ "$v" != "full" ]; then export FKS_LIB_OVERRIDE=$PWD/fate-llm_amd/build/libfks_$v.so; else unset FKS_LIB_OVERRIDE; fi
+  if [ "$v" != "full" ]; then export FKS_LIB_OVERRIDE=$PWD/fate-llm_amd/ab/libfks_$v.so; else unset FKS_LIB_OVERRIDE; fi
   i=0
   for g in "${GROUPS_[@]}"; do
     rm -rf gpurun_out/pmcsk_${v}_$i

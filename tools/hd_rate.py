@@ -9,6 +9,7 @@ Prints one JSON line.  Usage: python tools/hd_rate.py [--params N] [--ks 1,19,30
 import argparse
 import json
 import os
+os.environ.setdefault("FKS_STREAM_MODE", "torch_cpu")  # the CPU-generator stream these measurements use
 import sys
 import time
 

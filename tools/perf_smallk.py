@@ -7,6 +7,7 @@ python tools/perf_smallk.py [--params N] [--reps R]"""
 import argparse
 import json
 import os
+os.environ.setdefault("FKS_STREAM_MODE", "torch_cpu")  # the CPU-generator stream these measurements use
 import sys
 import time
 

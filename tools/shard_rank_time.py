@@ -8,6 +8,7 @@ python tools/shard_rank_time.py [--ns 1,2,4,8] [--wd 0.0] [--warm]"""
 import argparse
 import json
 import os
+os.environ.setdefault("FKS_STREAM_MODE", "torch_cpu")  # the CPU-generator stream these measurements use
 import sys
 import time
 
