@@ -15,6 +15,12 @@ the directional-derivative history.
 The federation context is duck-typed (``ctxs_range``, ``guest``, ``hosts``,
 ``arbiter.put/get``), so ``fate.arch`` is not a dependency of this package.
 
+The z stream (codec.py) is part of the round: a client logs the stream it draws and,
+over a ``payload.WireContext``, tags its histories with it; the arbiter rejects a
+history drawn from another stream than the rest of the federation's
+(``payload.StreamMismatchError``), since the reference's parties would otherwise apply
+one (seed, scalar) list along different directions without noticing.
+
 Round pipeline.  The reference rebuilds the model every round
 as ``copy.deepcopy(model_0).to(device)`` (fedkseed.py:132-133): a host copy of the
 whole buffer, then a pageable H2D copy.  The drop-in builds the device model directly:
@@ -34,7 +40,9 @@ from typing import Dict, List, Mapping, Optional
 
 import torch
 
+from . import codec
 from .args import KSeedTrainingArguments
+from .payload import WireContext, check_stream
 from .pytorch_utils import get_optimizer_parameters_grouped_with_decay
 from .zo_utils import get_even_seed_probabilities, probability_from_amps, reconstruct_
 
@@ -51,6 +59,9 @@ class Trainer:
         self.seed_candidates = seed_candidates
         self.k = len(seed_candidates)
         self.model = None
+        # the federation's z stream: what a WireContext declared, else the first tagged
+        # client history's; every later tagged history must match it
+        self.stream_mode = getattr(ctx, "stream_mode", None) if isinstance(ctx, WireContext) else None
 
     @staticmethod
     def get_clients(ctx) -> list:
@@ -85,8 +96,13 @@ class Trainer:
                 client.put("train_once", (False, payload))
             if sums is None:
                 sums = {s.item(): 0.0 for s in self.seed_candidates}
-            for client in clients:
-                for seed, values in client.get("direction_derivative_history").items():
+            for i, client in enumerate(clients):
+                hist = client.get("direction_derivative_history")
+                stream = getattr(hist, "stream_mode", None)  # payload.History of a tagged record
+                check_stream(self.stream_mode, stream, f"client {i} (guest first, then hosts)")
+                if self.stream_mode is None:
+                    self.stream_mode = stream
+                for seed, values in hist.items():
                     seed = int(seed)
                     history.setdefault(seed, []).extend(values)
                     # python float sum of the new values, then one float64 add; a seed
@@ -193,10 +209,22 @@ class ClientTrainer:
         self._pinned = False
         self._lock = threading.Lock()
 
+    @property
+    def stream_mode(self) -> str:
+        """The z stream this client's reconstruct and local steps draw: the process-wide
+        codec setting resolved for the training device (FKS_STREAM_MODE unset = "auto":
+        torch_rocm on an MI355X, what an unmodified reference client there draws)."""
+        return codec.resolve_stream_mode(getattr(self.training_args, "device", None))
+
     def train(self):
+        stream = self.stream_mode
+        logger.info(f"FedKSeed client: z stream {stream} (codec setting {codec.get_stream_mode()!r})")
+        if isinstance(self.ctx, WireContext):
+            self.ctx.declare_stream_mode(stream)  # tags the histories this client sends
         for i, sub_ctx in self.ctx.ctxs_range(self.fedkseed_args.num_aggregations):
             logger.info(f"training loop started: {i}")
             should_exit, kwargs = sub_ctx.arbiter.get("train_once")
+            check_stream(stream, kwargs.get("stream_mode"), "the arbiter")
             if should_exit:
                 break
             history = self.train_once(kwargs["seed_candidates"], kwargs["seed_probabilities"],

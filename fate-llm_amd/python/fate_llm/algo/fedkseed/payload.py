@@ -33,6 +33,16 @@ dtypes -- so the receiving ``Trainer``/``ClientTrainer`` code runs unchanged:
 / ``hosts`` / ``arbiter`` surface fedkseed.py uses) so those two keys travel encoded
 and every other key passes through untouched: opt-in, with no change to the trainers.
 
+**The z stream travels with the round.**  The reference draws z where the parameters
+live (zo_utils.py:47, optimizer.py:170-172: ``device=param.data.device``), so a party on
+a GPU and a party on the CPU apply the same (seed, scalar) list along different
+directions -- silently.  A record can carry the stream its
+sender draws (``stream_mode``: "torch_cpu" or "torch_rocm", two flag bits, no extra
+bytes): the drop-in ``ClientTrainer`` declares its stream into its ``WireContext``, the
+arbiter's ``Trainer`` rejects a history whose stream differs from the others'
+(``StreamMismatchError``), and a client rejects a "train_once" whose declared stream
+differs from its own.  Untagged records (a reference party) decode as before.
+
 Host-side logic only; it touches no parameters and no device.
 """
 import struct
@@ -56,6 +66,10 @@ _F_HAS_PROBS = 1 << 4
 _F_KEYS_I64 = 1 << 1
 _F_VALUES_F64 = 1 << 2
 _F_SPARSE = 1 << 3        # keys = the candidates: only (index, count) of non-empty lists
+# both kinds: the sender's z stream (bits 8-9, clear of every other flag)
+_F_STREAM_TAGGED = 1 << 8
+_F_STREAM_ROCM = 1 << 9
+STREAMS = ("torch_cpu", "torch_rocm")
 
 _HEADER = struct.Struct("<4sBBHQ")  # magic, version, kind, flags, count
 _U32_MAX = 2 ** 32
@@ -63,6 +77,40 @@ _U32_MAX = 2 ** 32
 
 class WireFormatError(ValueError):
     """A buffer that is not a valid FedKSeed wire record."""
+
+
+class StreamMismatchError(RuntimeError):
+    """Two parties of one federation draw different z streams (module docstring)."""
+
+
+class History(dict):
+    """A decoded ``direction_derivative_history``: the dict itself (equal to the
+    original), plus the ``stream_mode`` its sender declared (None if untagged)."""
+
+    stream_mode: Optional[str] = None
+
+
+def _stream_flags(stream_mode: Optional[str]) -> int:
+    if stream_mode is None:
+        return 0
+    if stream_mode not in STREAMS:
+        raise WireFormatError(f"stream_mode must be one of {STREAMS} or None, not {stream_mode!r}")
+    return _F_STREAM_TAGGED | (_F_STREAM_ROCM if stream_mode == "torch_rocm" else 0)
+
+
+def _stream_of(flags: int) -> Optional[str]:
+    if not flags & _F_STREAM_TAGGED:
+        return None
+    return "torch_rocm" if flags & _F_STREAM_ROCM else "torch_cpu"
+
+
+def check_stream(expected: Optional[str], got: Optional[str], what: str) -> None:
+    """Raise StreamMismatchError when both streams are known and differ."""
+    if expected is not None and got is not None and expected != got:
+        raise StreamMismatchError(
+            f"{what} draws the {got} z stream, this federation draws {expected}: the parties would apply "
+            "the same (seed, scalar) list along different directions (zo_utils.py:47 draws on the "
+            "parameters' device); set FKS_STREAM_MODE / codec.set_stream_mode alike on every party")
 
 
 def _keys_array(keys: Sequence[int]) -> Tuple[np.ndarray, bool]:
@@ -92,8 +140,9 @@ def _header(buf, kind: int) -> Tuple[memoryview, int, int]:
     return buf, flags, count
 
 
-def encode_train_once(message: Tuple[bool, Mapping]) -> bytes:
-    """``(should_exit, kwargs)`` of the arbiter's "train_once" put (fedkseed.py:66-68)."""
+def encode_train_once(message: Tuple[bool, Mapping], stream_mode: Optional[str] = None) -> bytes:
+    """``(should_exit, kwargs)`` of the arbiter's "train_once" put (fedkseed.py:66-68);
+    ``stream_mode``: the federation's z stream, if the arbiter declares one."""
     should_exit, kw = message
     seeds = kw["seed_candidates"]
     seeds_np = seeds.detach().cpu().numpy() if torch.is_tensor(seeds) else np.asarray(seeds)
@@ -102,7 +151,7 @@ def encode_train_once(message: Tuple[bool, Mapping]) -> bytes:
     probs = kw.get("seed_probabilities")
     sums: Optional[Mapping[int, float]] = kw.get("direction_derivative_sum")
 
-    flags = (_F_EXIT if should_exit else 0) | (_F_SEEDS_I64 if seeds_i64 else 0)
+    flags = (_F_EXIT if should_exit else 0) | (_F_SEEDS_I64 if seeds_i64 else 0) | _stream_flags(stream_mode)
     kdt = "<i8" if seeds_i64 else "<u4"
     parts = [seeds_arr.astype(kdt).tobytes()]
     if probs is not None:
@@ -128,7 +177,8 @@ def encode_train_once(message: Tuple[bool, Mapping]) -> bytes:
 
 def decode_train_once(buf) -> Tuple[bool, Dict]:
     """Inverse of ``encode_train_once``: seeds as ``torch.long``, probabilities as
-    ``torch.float32``, sums as a ``dict[int, float]`` in the encoded key order."""
+    ``torch.float32``, sums as a ``dict[int, float]`` in the encoded key order; a tagged
+    record adds ``"stream_mode"`` to the kwargs (the reference reads only its three keys)."""
     buf, flags, k = _header(buf, KIND_TRAIN_ONCE)
     off = _HEADER.size
     kdt = "<i8" if flags & _F_SEEDS_I64 else "<u4"
@@ -150,8 +200,10 @@ def decode_train_once(buf) -> Tuple[bool, Dict]:
         sums = dict(zip(keys, vals.tolist()))
     if off != len(buf):
         raise WireFormatError(f"{len(buf) - off} trailing bytes")
-    return bool(flags & _F_EXIT), {"seed_candidates": seed_t, "seed_probabilities": probs,
-                                   "direction_derivative_sum": sums}
+    kw = {"seed_candidates": seed_t, "seed_probabilities": probs, "direction_derivative_sum": sums}
+    if _stream_of(flags) is not None:
+        kw["stream_mode"] = _stream_of(flags)
+    return bool(flags & _F_EXIT), kw
 
 
 def _values_block(flat: np.ndarray) -> Tuple[int, bytes]:
@@ -161,10 +213,13 @@ def _values_block(flat: np.ndarray) -> Tuple[int, bytes]:
     return (0 if lossless else _F_VALUES_F64), (as32 if lossless else flat).tobytes()
 
 
-def encode_history(history: Mapping[int, Sequence[float]], candidates: Optional[Sequence[int]] = None) -> bytes:
+def encode_history(history: Mapping[int, Sequence[float]], candidates: Optional[Sequence[int]] = None,
+                   stream_mode: Optional[str] = None) -> bytes:
     """A client's ``direction_derivative_history`` (dict seed -> list of g values).
     ``candidates``: the round's seed candidates, known to both ends -- enables the
-    sparse form when the history's keys are exactly these seeds in order."""
+    sparse form when the history's keys are exactly these seeds in order.
+    ``stream_mode``: the z stream the client drew its steps from (tags the record)."""
+    sflags = _stream_flags(stream_mode)
     keys = [int(s) for s in history.keys()]
     counts = np.fromiter((len(v) for v in history.values()), dtype="<u4", count=len(keys))
     flat = np.fromiter((float(x) for v in history.values() for x in v), dtype="<f8",
@@ -172,15 +227,17 @@ def encode_history(history: Mapping[int, Sequence[float]], candidates: Optional[
     vflag, vbytes = _values_block(flat)
     if candidates is not None and keys == [int(c) for c in candidates]:
         nz = np.nonzero(counts)[0]
-        return (_HEADER.pack(MAGIC, VERSION, KIND_HISTORY, _F_SPARSE | vflag, len(nz))
+        return (_HEADER.pack(MAGIC, VERSION, KIND_HISTORY, _F_SPARSE | vflag | sflags, len(nz))
                 + nz.astype("<u4").tobytes() + counts[nz].tobytes() + vbytes)
     karr, ki64 = _keys_array(keys)
-    flags = (_F_KEYS_I64 if ki64 else 0) | vflag
+    flags = (_F_KEYS_I64 if ki64 else 0) | vflag | sflags
     return (_HEADER.pack(MAGIC, VERSION, KIND_HISTORY, flags, len(keys))
             + karr.astype("<i8" if ki64 else "<u4").tobytes() + counts.tobytes() + vbytes)
 
 
 def decode_history(buf, candidates: Optional[Sequence[int]] = None) -> Dict[int, List[float]]:
+    """Inverse of ``encode_history``; a tagged record decodes to a ``History`` carrying
+    the sender's ``stream_mode``."""
     buf, flags, n = _header(buf, KIND_HISTORY)
     off = _HEADER.size
     if flags & _F_SPARSE:
@@ -195,7 +252,10 @@ def decode_history(buf, candidates: Optional[Sequence[int]] = None) -> Dict[int,
     if off != len(buf):
         raise WireFormatError(f"{len(buf) - off} trailing bytes")
     flat = vals.astype(np.float64).tolist()
-    out: Dict[int, List[float]] = {}
+    stream = _stream_of(flags)
+    out: Dict[int, List[float]] = {} if stream is None else History()
+    if stream is not None:
+        out.stream_mode = stream
     pos = 0
     if flags & _F_SPARSE:
         cand = [int(c) for c in candidates]
@@ -205,7 +265,8 @@ def decode_history(buf, candidates: Optional[Sequence[int]] = None) -> Dict[int,
         for i, c in zip(idx.tolist(), counts.tolist()):
             got[i] = flat[pos:pos + c]
             pos += c
-        return {s: got.get(i, []) for i, s in enumerate(cand)}
+        out.update((s, got.get(i, [])) for i, s in enumerate(cand))
+        return out
     for key, c in zip(keys.astype(np.int64).tolist(), counts.tolist()):
         out[key] = flat[pos:pos + c]
         pos += c
@@ -215,17 +276,19 @@ def decode_history(buf, candidates: Optional[Sequence[int]] = None) -> Dict[int,
 class _WireParty:
     """One federation party (``ctx.guest`` / a host / ``ctx.arbiter``) whose FedKSeed
     keys are encoded on ``put`` and decoded on ``get``.  The link remembers the seed
-    candidates of its last "train_once" (either direction) for the sparse history."""
+    candidates of its last "train_once" (either direction) for the sparse history, and
+    tags what it sends with the stream its context declared."""
 
     def __init__(self, party, state, role):
         self._party, self._state, self._role = party, state, role
 
     def put(self, key, value):
+        stream = self._state.get(_STREAM_KEY)
         if key == "train_once":
             self._state[self._role] = [int(s) for s in value[1]["seed_candidates"]]
-            value = encode_train_once(value)
+            value = encode_train_once(value, stream)
         elif key == "direction_derivative_history":
-            value = encode_history(value, self._state.get(self._role))
+            value = encode_history(value, self._state.get(self._role), stream)
         return self._party.put(key, value)
 
     def get(self, key):
@@ -235,6 +298,7 @@ class _WireParty:
         if key == "train_once":
             value = decode_train_once(value)
             self._state[self._role] = value[1]["seed_candidates"].tolist()
+            check_stream(self._state.get(_STREAM_KEY), value[1].get("stream_mode"), "the arbiter")
         elif key == "direction_derivative_history":
             value = decode_history(value, self._state.get(self._role))
         return value
@@ -243,14 +307,30 @@ class _WireParty:
         return getattr(self._party, name)
 
 
+_STREAM_KEY = object()  # WireContext state: the z stream this party declared
+
+
 class WireContext:
     """Wraps a federation context: ``ctxs_range`` yields wrapped sub-contexts whose
     ``guest``, ``hosts`` and ``arbiter`` parties move the FedKSeed round payloads in
-    the compact format.  Both ends of a link must be wrapped."""
+    the compact format.  Both ends of a link must be wrapped.  ``stream_mode``: the z
+    stream this party draws ("torch_cpu" / "torch_rocm"), carried by every record it
+    sends; the drop-in ClientTrainer declares its own (``declare_stream_mode``)."""
 
-    def __init__(self, ctx, _state=None):
+    def __init__(self, ctx, _state=None, stream_mode: Optional[str] = None):
         self._ctx = ctx
         self._state = {} if _state is None else _state  # role -> seed candidates of the link
+        if stream_mode is not None:
+            self.declare_stream_mode(stream_mode)
+
+    def declare_stream_mode(self, stream_mode: Optional[str]) -> None:
+        _stream_flags(stream_mode)  # validates
+        check_stream(self._state.get(_STREAM_KEY), stream_mode, "this party")
+        self._state[_STREAM_KEY] = stream_mode
+
+    @property
+    def stream_mode(self) -> Optional[str]:
+        return self._state.get(_STREAM_KEY)
 
     def ctxs_range(self, n):
         for i, sub in self._ctx.ctxs_range(n):

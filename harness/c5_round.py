@@ -16,6 +16,11 @@ round payloads through the drop-in classes:
     directly (2 perturbations + 1 fused restore/update per step, K=1 codec calls).
   * ``--wire``: both ends wrap their context in payload.WireContext, so the round
     payloads travel in the compact binary format; bytes per round are reported.
+  * ``--record`` (parity instrumentation, tests/test_gpu_c5_harness.py): each client also
+    returns its model_0 prefix, and per round the payload it received, the first 4096
+    parameters after the reconstruct and after the local steps, and its local steps in
+    order (sampled seed, g, group-0 lr), so every client's round can be replayed through
+    the oracle.
 
 The FATE transport is out of scope: payloads move as pickled objects
 over a torch.distributed gloo group (CPU), the duck-typed context the drop-in Trainer /
@@ -157,8 +162,18 @@ class _Steps(torch.utils.data.Dataset):
         return {"input_ids": torch.zeros(1, dtype=torch.long)}
 
 
+PREFIX = 4096  # parameters of the first tensor a --record client reports
+
+
+def _prefix_bits(model):
+    """The first PREFIX elements of the model's first parameter, as raw bits (bf16: u16)."""
+    t = next(model.parameters()).detach().reshape(-1)[:PREFIX]
+    return t.view(torch.int16).cpu().numpy().view("u2").tolist()
+
+
 def run_client(rank, args, arbiter_rank):
     from fate_llm.algo.fedkseed import fedkseed as F
+    from fate_llm.algo.fedkseed import optimizer as OPT
     from fate_llm.algo.fedkseed.optimizer import KSeedZerothOrderOptimizer
     from fate_llm.algo.fedkseed.payload import WireContext
     from fate_llm.algo.fedkseed.pytorch_utils import get_optimizer_parameters_grouped_with_decay
@@ -172,6 +187,18 @@ def run_client(rank, args, arbiter_rank):
     raw = _Ctx([], arbiter_rank)
     ctx = WireContext(raw) if args.wire else raw
     timings, received_all, histories = [], [], []
+    records = {"model_0": _prefix_bits(model_0), "rounds": []} if args.record else None
+    steps = []  # this round's local steps: (seed, g as returned -- a device or host value --, group-0 lr)
+    if args.record:
+        orig_step = OPT.ZerothOrderOptimizer.zeroth_order_step
+
+        def recorded_step(self, seed, closure):
+            lr = self.param_groups[0]["lr"]  # the sticky lr of the step's update (zo_utils.py:44-45)
+            out = orig_step(self, seed, closure)
+            steps.append((int(seed), out[0], float(lr)))
+            return out
+
+        OPT.ZerothOrderOptimizer.zeroth_order_step = recorded_step
 
     if args.driver == "trainer":
         import tempfile
@@ -192,6 +219,7 @@ def run_client(rank, args, arbiter_rank):
 
         def reconstruct(self, sums):
             received_all.append(None if sums is None else {int(k): float(v) for k, v in sums.items()})
+            steps.clear()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             model = self.materialize()
@@ -205,6 +233,9 @@ def run_client(rank, args, arbiter_rank):
             torch.cuda.synchronize()
             self._t = {"t0": t0, "materialize_s": t1 - t0, "reconstruct_s": time.perf_counter() - t1,
                        "seeds_reconstructed": n}
+            if records is not None:
+                self._model = model
+                self._after_reconstruct = _prefix_bits(model)
             return model
 
         def train_once(self, seed_candidates, seed_probabilities, direction_derivative_sum):
@@ -238,6 +269,16 @@ def run_client(rank, args, arbiter_rank):
             timings.append(rec)
             hist = {int(s): list(v) for s, v in hist.items()}
             histories.append(hist)
+            if records is not None:
+                records["rounds"].append({
+                    "sums": received_all[-1],
+                    "candidates": [int(x) for x in seed_candidates],
+                    "probabilities": torch.as_tensor(seed_probabilities).float().tolist(),
+                    "after_reconstruct": self._after_reconstruct,
+                    "steps": [(sd, float(torch.as_tensor(g).reshape(()).item()), lr) for sd, g, lr in steps],
+                    "after_steps": _prefix_bits(self._model),
+                    "history": hist})
+                self._model = None
             return hist
 
     trainer = TimedClient(ctx, model_0, fk, training_args, _Steps(args.steps) if args.driver == "trainer" else None,
@@ -245,7 +286,7 @@ def run_client(rank, args, arbiter_rank):
     trainer.train()
     small = args.k <= 256
     return {"rounds": timings, "received_sums": received_all if small else None,
-            "histories": histories if small else None, "bytes": raw.meter}
+            "histories": histories if small else None, "bytes": raw.meter, "records": records}
 
 
 # ----------------------------------------------------------------------------- aggregator
@@ -326,6 +367,7 @@ def main(argv=None):
                     help="ClientTrainer model_0_placement")
     ap.add_argument("--driver", choices=("optimizer", "trainer"), default="optimizer")
     ap.add_argument("--wire", action="store_true", help="round payloads in the compact binary format")
+    ap.add_argument("--record", action="store_true", help="return every client's round for an oracle replay")
     args = ap.parse_args(argv)
     if args.resident:
         args.placement = "device"
@@ -365,6 +407,8 @@ def main(argv=None):
            "client_received_sums": {c["client"]: c["received_sums"] for c in clients} if args.k <= 256 else None,
            "client_histories": {c["client"]: c["histories"] for c in clients} if args.k <= 256 else None}
     print(json.dumps(out), flush=True)
+    if args.record:  # returned, not printed (8 clients x 3 rounds x 3 prefixes)
+        out["client_records"] = {c["client"]: c["records"] for c in clients}
     return out
 
 

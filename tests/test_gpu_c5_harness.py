@@ -8,9 +8,21 @@ aggregator process exchange the drop-in Trainer / ClientTrainer payloads over gl
   through KSeedZOExtendedTrainer.training_step in the transformers loop, payloads in the
   compact wire format: what every client received each round equals what the drop-in
   arbiter computes offline from the same client histories (fedkseed.py:41-85), and the
-  histories travel as a few hundred bytes."""
+  histories travel as a few hundred bytes;
+* the same run replayed, client by client and round by round, through the oracle: the
+  reconstruct from model_0 of the cumulative (seed, sum) list (fedkseed.py:130-141), then
+  every local step -- perturb +eps, -2 eps, +eps, the update with g (optimizer.py:108-150,
+  :210-235) -- must give the client's first 4096 parameters bit for bit after the
+  reconstruct and after the local steps; each g must be the loss difference of the
+  oracle's perturbed parameters (the synthetic closure recomputed in float64), and each
+  client's history must be its steps' g in order."""
+import math
+
+import numpy as np
 import pytest
 import torch
+
+from oracle import fks_oracle as O
 
 pytestmark = pytest.mark.gpu
 
@@ -32,7 +44,7 @@ def test_eight_clients_trainer_loop_wire():
     from harness import c5_round
     rounds, k, steps = 3, 64, 5
     out = c5_round.main(["--params", "262144", "--k", str(k), "--steps", str(steps), "--rounds", str(rounds),
-                         "--clients", "8", "--driver", "trainer", "--wire", "--placement", "pinned"])
+                         "--clients", "8", "--driver", "trainer", "--wire", "--placement", "pinned", "--record"])
     assert len(out["rounds"]) == rounds
     got = out["client_received_sums"]
     assert len(got) == 8
@@ -78,3 +90,106 @@ def test_eight_clients_trainer_loop_wire():
     b = out["bytes_per_round_per_client"]
     assert b["direction_derivative_history.recv"] < 400
     assert out["rounds"][1]["seeds_reconstructed"] >= 1
+
+    # ---- the offline arbiter's probabilities too: what each client received, bit for bit,
+    # shaped as the reference's payload (tests/golden/cases.json "server": K candidates, K
+    # float32 probabilities, the sums keyed by the candidates in order, None in round 0)
+    recs = out["client_records"]
+    seeds = [int(x) for x in out["seeds"]]
+    for c, client in zip(sorted(got), cl):
+        for r, rnd in enumerate(recs[c]["rounds"]):
+            assert rnd["candidates"] == seeds
+            assert len(rnd["probabilities"]) == k
+            assert np.float32(sum(rnd["probabilities"])) == pytest.approx(1.0, abs=1e-5)
+            assert (rnd["sums"] is None) == (r == 0)
+            if rnd["sums"] is not None:
+                assert [int(x) for x in rnd["sums"]] == seeds
+    probs_sent = _offline_probabilities(hists, out["seeds"], rounds, k)
+    for c in sorted(got):
+        assert [rnd["probabilities"] for rnd in recs[c]["rounds"]] == probs_sent
+
+    # ---- every client's rounds through the oracle
+    checked = 0
+    for c in sorted(recs):
+        checked += _replay_client(recs[c], steps)
+    assert checked == 8 * rounds * steps
+
+
+def _offline_probabilities(hists, seeds, rounds, k):
+    from fate_llm.algo.fedkseed.fedkseed import FedKSeedTrainingArguments, Trainer
+
+    class Client:
+        def __init__(self, replies):
+            self.replies, self.probs = list(replies), []
+
+        def put(self, key, value):
+            self.probs.append(value[1]["seed_probabilities"].tolist())
+
+        def get(self, key):
+            return self.replies.pop(0)
+
+    class Ctx:
+        def __init__(self, cl):
+            self.guest, self.hosts = cl[0], cl[1:]
+
+        def ctxs_range(self, n):
+            for i in range(n):
+                yield i, self
+
+    cl = [Client([{int(s): v for s, v in h.items()} for h in hists[c]]) for c in sorted(hists)]
+    Trainer(Ctx(cl), torch.tensor(seeds, dtype=torch.long), None, FedKSeedTrainingArguments(num_aggregations=rounds, k=k)).train()
+    assert all(x.probs == cl[0].probs for x in cl)
+    return cl[0].probs
+
+
+def _bf16_value(x: float) -> float:
+    """A 0-dim f32 g as the reference's bf16 update sees it: cast to the parameter dtype
+    (zo_utils._value_kind), RNE."""
+    return float(torch.tensor(x, dtype=torch.float32).to(torch.bfloat16).float())
+
+
+def _loss64(bits: np.ndarray) -> float:
+    """harness SyntheticModel.forward on the prefix: mean(p^2) * 1e3, in float64."""
+    v = (bits.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+    return float(np.mean(v * v) * 1e3)
+
+
+def _replay_client(rec, steps_per_round, eps=5e-4, lr_reconstruct=1e-5):
+    """Replay one client's rounds through the oracle (bf16, the prefix of its one flat
+    tensor: a 262,144-element tensor's first 4096 z are a 4096-element tensor's); returns
+    the number of local steps checked."""
+    model_0 = np.array(rec["model_0"], dtype=np.uint16)
+    n = 0
+    for r, rnd in enumerate(rec["rounds"]):
+        p = model_0.copy()  # every round restarts from model_0 (fedkseed.py:132)
+        sums = rnd["sums"]
+        if sums:
+            keep = [(int(s), v) for s, v in sums.items() if v != 0.0]
+            # ClientTrainer passes training_args' lr and weight decay (0.0) explicitly (:138-141)
+            O.reconstruct([p], [O.BF16], [lr_reconstruct], [0.0], [s for s, _ in keep], [v for _, v in keep])
+        got = np.array(rnd["after_reconstruct"], dtype=np.uint16)
+        assert np.array_equal(got, p), f"round {r}: reconstruct differs from the oracle at {int(np.argmax(got != p))}"
+        hist = {}
+        assert len(rnd["steps"]) == steps_per_round
+        for seed, g, lr in rnd["steps"]:
+            O.perturb_params([p], [O.BF16], seed, 1.0 * eps)
+            loss_right = _loss64(p)
+            O.perturb_params([p], [O.BF16], seed, -2.0 * eps)
+            loss_left = _loss64(p)
+            O.perturb_params([p], [O.BF16], seed, 1.0 * eps)
+            assert not math.isnan(g)  # the synthetic closure's losses are finite
+            g64 = (loss_right - loss_left) / (2 * eps)
+            # g = (L+ - L-) / (2 eps) of the very parameters the oracle holds: the GPU
+            # evaluates the closure in f32, so compare within its rounding of the losses
+            assert abs(g - g64) <= 2e-3 * abs(g64) + 2e-3, (r, seed, g, g64)
+            # local update: the sticky group-0 lr and weight decay 0.0 (zo_utils.py:44-45);
+            # the 0-dim f32 g is cast to bf16 by the reference's g * z
+            O.reconstruct([p], [O.BF16], [lr], [0.0], [seed], [_bf16_value(g)])
+            hist.setdefault(seed, []).append(g)
+            n += 1
+        got = np.array(rnd["after_steps"], dtype=np.uint16)
+        assert np.array_equal(got, p), f"round {r}: local steps differ from the oracle at {int(np.argmax(got != p))}"
+        h = {int(s): v for s, v in rnd["history"].items()}
+        assert {s: v for s, v in h.items() if v} == hist
+        assert list(h) == rnd["candidates"]
+    return n

@@ -1,0 +1,187 @@
+"""The z stream as an explicit, checked part of a FedKSeed round (CPU, no device).
+
+The reference draws z where the parameters live (zo_utils.py:47, optimizer.py:170-172:
+``device=param.data.device``, after ``model.to(training_args.device)`` at fedkseed.py:133),
+so a reference client on an MI355X draws torch's HIP-generator (Philox) stream and one on
+the CPU draws mt19937.  What these tests pin:
+
+* ``FKS_STREAM_MODE`` unset means "auto": the stream the reference draws on the tensors'
+  device -- torch_rocm for a client whose ``training_args.device`` is cuda, so the drop-in
+  and an unmodified reference client on the same GPU give the same bits;
+* the wire records carry the sender's stream (two flag bits) and decode to objects equal
+  to the originals;
+* two clients on different streams make the drop-in arbiter fail loudly, and a client
+  refuses an arbiter that declared another stream.
+"""
+import os
+import queue
+import subprocess
+import sys
+import threading
+
+import pytest
+import torch
+
+from fate_llm.algo.fedkseed import codec
+from fate_llm.algo.fedkseed import fedkseed as F
+from fate_llm.algo.fedkseed import payload as W
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture
+def setting():
+    old = codec.get_stream_mode()
+    yield codec.set_stream_mode
+    codec.set_stream_mode(old)
+
+
+def test_unset_env_means_auto_which_follows_the_device():
+    env = {k: v for k, v in os.environ.items() if k != "FKS_STREAM_MODE"}
+    code = ("import sys; sys.path.insert(0, 'fate-llm_amd/python'); import torch\n"
+            "from fate_llm.algo.fedkseed import codec\n"
+            "print(codec.get_stream_mode(), codec.resolve_stream_mode(torch.device('cuda', 0)), "
+            "codec.resolve_stream_mode('cpu'), codec.resolve_stream_mode(None))")
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, check=True)
+    assert out.stdout.split() == ["auto", "torch_rocm", "torch_cpu", "torch_cpu"]
+
+
+def test_resolve_stream_mode(setting):
+    setting("auto")
+    assert codec.resolve_stream_mode("cuda:1") == "torch_rocm"
+    assert codec.resolve_stream_mode(torch.device("cpu")) == "torch_cpu"
+    assert codec.resolve_stream_mode("cuda", stream_mode="torch_cpu") == "torch_cpu"
+    setting("torch_cpu")
+    assert codec.resolve_stream_mode("cuda") == "torch_cpu"
+    assert codec.resolve_stream_mode("cuda", stream_mode="auto") == "torch_rocm"
+    with pytest.raises(ValueError):
+        codec.resolve_stream_mode("cuda", stream_mode="philox")
+    with pytest.raises(ValueError):
+        setting("mt19937")
+
+
+class _Args:
+    learning_rate, weight_decay = 1e-5, 0.0
+
+    def __init__(self, device):
+        self.device = device
+
+
+def test_client_stream_follows_training_device(setting):
+    setting("auto")
+    gpu = F.ClientTrainer(None, torch.nn.Linear(2, 2), F.FedKSeedTrainingArguments(), _Args("cuda:0"),
+                          None, None, None, None)
+    cpu = F.ClientTrainer(None, torch.nn.Linear(2, 2), F.FedKSeedTrainingArguments(), _Args(torch.device("cpu")),
+                          None, None, None, None)
+    assert (gpu.stream_mode, cpu.stream_mode) == ("torch_rocm", "torch_cpu")
+    setting("torch_cpu")  # an explicit setting wins on any device
+    assert gpu.stream_mode == "torch_cpu"
+
+
+def test_wire_records_carry_the_stream():
+    cands = [3, 1 << 31, 7]
+    hist = {3: [0.25, -1.5], 1 << 31: [], 7: [2.0]}
+    for stream in ("torch_cpu", "torch_rocm"):
+        for c in (cands, None):  # sparse and explicit-key forms
+            back = W.decode_history(W.encode_history(hist, c, stream), c)
+            assert isinstance(back, W.History) and back == hist and back.stream_mode == stream
+            assert list(back) == list(hist)
+    plain = W.decode_history(W.encode_history(hist, cands), cands)
+    assert type(plain) is dict and plain == hist and getattr(plain, "stream_mode", None) is None
+    # the tag costs no bytes
+    assert len(W.encode_history(hist, cands, "torch_rocm")) == len(W.encode_history(hist, cands))
+    msg = (False, {"seed_candidates": torch.tensor(cands), "seed_probabilities": torch.ones(3) / 3,
+                   "direction_derivative_sum": {3: 1.0, 1 << 31: 0.0, 7: -2.0}})
+    ex, kw = W.decode_train_once(W.encode_train_once(msg, "torch_rocm"))
+    assert kw["stream_mode"] == "torch_rocm" and kw["direction_derivative_sum"] == msg[1]["direction_derivative_sum"]
+    ex, kw = W.decode_train_once(W.encode_train_once(msg))
+    assert "stream_mode" not in kw
+    with pytest.raises(W.WireFormatError):
+        W.encode_history(hist, cands, "mt")
+
+
+# --------------------------------------------------------------- a loopback federation
+class _Party:
+    def __init__(self, out_q, in_q):
+        self.out_q, self.in_q = out_q, in_q
+
+    def put(self, key, value):
+        self.out_q.put((key, value))
+
+    def get(self, key):
+        k, v = self.in_q.get(timeout=5)
+        assert k == key, (k, key)
+        return v
+
+
+class _ArbiterCtx:
+    def __init__(self, links):
+        self.guest = _Party(links[0][0], links[0][1])
+        self.hosts = [_Party(a, b) for a, b in links[1:]]
+
+    def ctxs_range(self, n):
+        for i in range(n):
+            yield i, self
+
+
+class _ClientCtx:
+    def __init__(self, link):
+        self.arbiter = _Party(link[1], link[0])
+
+    def ctxs_range(self, n):
+        for i in range(n):
+            yield i, self
+
+
+class _ScalarClient(F.ClientTrainer):
+    """The drop-in ClientTrainer's round loop with a host-only local phase: one g for the
+    first sampled candidate (the codec is not needed to exercise the protocol)."""
+
+    def train_once(self, seed_candidates, seed_probabilities, direction_derivative_sum):
+        first = int(seed_candidates[0])
+        return {int(s): ([0.5] if int(s) == first else []) for s in seed_candidates}
+
+
+def _federation(devices, arbiter_stream=None, rounds=1):
+    links = [(queue.Queue(), queue.Queue()) for _ in devices]
+    errors, threads = {}, []
+
+    def run(name, fn):
+        try:
+            fn()
+        except Exception as e:  # noqa: BLE001 -- reported to the test
+            errors[name] = e
+
+    arb = F.Trainer(W.WireContext(_ArbiterCtx(links), stream_mode=arbiter_stream), torch.tensor([11, 22, 33]),
+                    None, F.FedKSeedTrainingArguments(num_aggregations=rounds, k=3))
+    threads.append(threading.Thread(target=run, args=("arbiter", arb.train), daemon=True))
+    for i, (dev, link) in enumerate(zip(devices, links)):
+        cl = _ScalarClient(W.WireContext(_ClientCtx(link)), torch.nn.Linear(2, 2),
+                           F.FedKSeedTrainingArguments(num_aggregations=rounds), _Args(dev), None, None, None, None)
+        threads.append(threading.Thread(target=run, args=(f"client{i}", cl.train), daemon=True))
+    for t in threads:
+        t.start()
+    threads[0].join(timeout=30)
+    assert not threads[0].is_alive()
+    return arb, errors
+
+
+def test_same_stream_federation_runs(setting):
+    setting("auto")
+    arb, errors = _federation(["cuda:0", "cuda:0", "cuda:1"], rounds=2)
+    assert not errors
+    assert arb.stream_mode == "torch_rocm"
+
+
+def test_clients_on_different_streams_fail_loudly(setting):
+    setting("auto")  # guest and host 1 on a GPU (torch_rocm), host 2 on the CPU (torch_cpu)
+    arb, errors = _federation(["cuda:0", "cuda:0", "cpu"])
+    assert isinstance(errors.get("arbiter"), W.StreamMismatchError)
+    assert "client 2" in str(errors["arbiter"]) and "torch_cpu" in str(errors["arbiter"])
+
+
+def test_client_refuses_an_arbiter_on_another_stream(setting):
+    setting("torch_rocm")
+    arb, errors = _federation(["cuda:0"], arbiter_stream="torch_cpu")
+    assert isinstance(errors.get("client0"), W.StreamMismatchError)
+    assert "the arbiter" in str(errors["client0"])
