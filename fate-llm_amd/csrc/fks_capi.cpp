@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cctype>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -794,6 +795,17 @@ ZCache* z_entry() {
   return Z;
 }
 
+// A boolean switch of the environment: on for 1 / true / yes / on (any case), off when
+// unset, empty or anything else -- so FKS_NO_JWIN=0 leaves the cache ON (codec._env_on
+// reads the same values).
+bool env_on(const char* name) {
+  const char* e = std::getenv(name);
+  if (!e) return false;
+  std::string v(e);
+  for (char& ch : v) ch = (char)std::tolower((unsigned char)ch);
+  return v == "1" || v == "true" || v == "yes" || v == "on";
+}
+
 // The z-index cache of the current device, ordered after its last user on `stream`, if
 // the attached buffer holds `bytes`; nullptr otherwise (the call then generates).
 ZCache* z_cache(void* stream, size_t bytes) {
@@ -830,7 +842,7 @@ JWin* jw_entry() {
 // pairs on `stream`, ordered after its last user, or nullptr (none attached, or too small
 // for one two-slice pass).  A new key drops every set.
 JWin* jw_cache(void* stream, uint64_t key, int nch) {
-  if (std::getenv("FKS_NO_JWIN")) return nullptr;
+  if (env_on("FKS_NO_JWIN")) return nullptr;
   JWin* J = jw_entry();
   if (!J || !J->buf) return nullptr;
   const size_t set_bytes = sizeof(uint32_t) * (size_t)kMtN * (size_t)nch;
@@ -888,7 +900,7 @@ void jw_assign(JWin* J, const uint64_t* seeds, int nb, uint32_t* slot, uint64_t*
 // `bytes` (ordered after the buffer's last user), or nullptr when it cannot be used
 // (FKS_NO_WIN_CACHE set, or no memory: the call then jumps into its workspace).
 WinCache* win_cache(void* stream, size_t bytes) {
-  if (std::getenv("FKS_NO_WIN_CACHE")) return nullptr;
+  if (env_on("FKS_NO_WIN_CACHE")) return nullptr;
   int dev = 0;
   (void)hipGetDevice(&dev);
   WinCache* W = nullptr;
@@ -939,16 +951,10 @@ int jump_chunks_per_wg(int nseeds, int nchunks) {
 // device once per distinct tensor list (same key as the MT plans, bounded LRU, freed by
 // fks_plan_cache_clear).  The geometry is torch's calc_execution_policy
 // (ATen/native/cuda/DistributionTemplates.h:50-62) on this device.
-PhxPlan* get_phx_plan(const fks_tensor* t, int nt, const double* scales) {
-  std::vector<uint8_t> key = plan_key(t, nt, scales, 0, 0, 1, false);
-  key_put(key, (int)0x7068);  // "ph": not an MT plan key
-  key_put(key, device_max_threads_per_cu());
-  const uint64_t h = fnv1a(key);
-  for (PhxPlan* P : g_phx)
-    if (P->hash == h && P->key == key) {
-      P->last_use = ++g_cache_clock;
-      return P;
-    }
+// The table and geometry alone, on the host (nothing cached, nothing uploaded): what
+// fks_shard_census reads; get_phx_plan adds the device copy.  Needs a current device
+// (its CU count and threads per CU set torch's grid).
+void phx_geometry(const fks_tensor* t, int nt, const double* scales, PhxPlan* P) {
   const int64_t max_grid = (int64_t)device_cu_count() * (device_max_threads_per_cu() / 256);
   std::vector<PhxTensor> tab;
   std::vector<int64_t> elem0;
@@ -982,10 +988,6 @@ PhxPlan* get_phx_plan(const fks_tensor* t, int nt, const double* scales) {
     }
     off4 += (uint64_t)J;
   }
-  auto* P = new PhxPlan();
-  P->key = std::move(key);
-  P->hash = h;
-  P->last_use = ++g_cache_clock;
   P->nt = (int)tab.size();
   P->items = items;
   P->elems = elems;
@@ -999,19 +1001,42 @@ PhxPlan* get_phx_plan(const fks_tensor* t, int nt, const double* scales) {
     else if (!tab.empty() && nwd == tab.size()) P->wd_mode = kModeUpdateWd;
     else if (!tab.empty() && nwd == 0) P->wd_mode = kModeUpdateNoWd;
   }
+  P->tab = std::move(tab);
+  P->elem0 = std::move(elem0);
+}
+
+PhxPlan* get_phx_plan(const fks_tensor* t, int nt, const double* scales) {
+  std::vector<uint8_t> key = plan_key(t, nt, scales, 0, 0, 1, false);
+  key_put(key, (int)0x7068);  // "ph": not an MT plan key
+  key_put(key, device_max_threads_per_cu());
+  const uint64_t h = fnv1a(key);
+  for (PhxPlan* P : g_phx)
+    if (P->hash == h && P->key == key) {
+      P->last_use = ++g_cache_clock;
+      return P;
+    }
+  auto* P = new PhxPlan();
+  try {
+    phx_geometry(t, nt, scales, P);
+  } catch (...) {
+    delete P;
+    throw;
+  }
+  P->key = std::move(key);
+  P->hash = h;
+  P->last_use = ++g_cache_clock;
   (void)hipGetDevice(&P->device);
-  const size_t bytes = std::max<size_t>(sizeof(PhxTensor) * tab.size(), 256);
+  const size_t bytes = std::max<size_t>(sizeof(PhxTensor) * P->tab.size(), 256);
   if (hipMalloc(&P->dev, bytes) != hipSuccess) {
     delete P;
     throw Error(-FKS_ENOMEM, "torch_rocm plan hipMalloc");
   }
-  if (!tab.empty() && hipMemcpy(P->dev, tab.data(), sizeof(PhxTensor) * tab.size(), hipMemcpyHostToDevice) != hipSuccess) {
+  if (!P->tab.empty() &&
+      hipMemcpy(P->dev, P->tab.data(), sizeof(PhxTensor) * P->tab.size(), hipMemcpyHostToDevice) != hipSuccess) {
     (void)hipFree(P->dev);
     delete P;
     throw Error(-FKS_EHIP, "torch_rocm plan upload");
   }
-  P->tab = std::move(tab);
-  P->elem0 = std::move(elem0);
   if (g_phx.size() >= kPlanCacheEntries) {
     auto victim = std::min_element(g_phx.begin(), g_phx.end(),
                                    [](const PhxPlan* a, const PhxPlan* b) { return a->last_use < b->last_use; });
@@ -1385,18 +1410,24 @@ int fks_zindex_attach(void* buf, size_t bytes) {
   });
 }
 
-int fks_jwin_size(const fks_tensor* t, int32_t nt, int32_t k, size_t* bytes) {
+int fks_jwin_size_shard(const fks_tensor* t, int32_t nt, int32_t k, int32_t shard, int32_t nshards, size_t* bytes) {
   return guarded([&] {
     validate(t, nt);
     if (!bytes || k < 0) throw Error(-FKS_EINVAL, "bad arguments");
+    if (nshards < 1 || shard < 0 || shard >= nshards) throw Error(-FKS_EINVAL, "bad shard");
     *bytes = 0;
     if (rocm_stream(t, nt) || k <= kBsSeeds) return;  // the Philox stream jumps nothing
     std::lock_guard<std::mutex> lk(g_cache_mu);
-    const CachedPlan* C = get_plan(t, nt, nullptr, 0, 0, 1, false);
+    // the plan the sharded call itself launches with (run() keys jw_cache on its chunks)
+    const CachedPlan* C = get_plan(t, nt, nullptr, 0, shard, nshards, false);
     if (!C->have_bs) return;
     const size_t set_bytes = sizeof(uint32_t) * (size_t)kMtN * (size_t)(C->Z.bs_chunks / kBsChunksPerWg);
     *bytes = set_bytes * (size_t)std::max(k, kBsPassSeeds);
   });
+}
+
+int fks_jwin_size(const fks_tensor* t, int32_t nt, int32_t k, size_t* bytes) {
+  return fks_jwin_size_shard(t, nt, k, 0, 1, bytes);
 }
 
 int fks_jwin_attach(void* buf, size_t bytes) {
@@ -1528,8 +1559,11 @@ int fks_shard_census(const fks_tensor* t, int32_t nt, int32_t shard, int32_t nsh
     validate(t, nt);
     if (nshards < 1 || shard < 0 || shard >= nshards) throw Error(-FKS_EINVAL, "bad shard");
     if (rocm_stream(t, nt)) {  // element runs of whole Philox rows (phx_boundary)
-      std::lock_guard<std::mutex> lk(g_cache_mu);
-      const PhxPlan* P = get_phx_plan(t, nt, nullptr);
+      // host geometry only: no plan cache entry, no device allocation (the scales do not
+      // move row boundaries)
+      PhxPlan geo;
+      phx_geometry(t, nt, nullptr, &geo);
+      const PhxPlan* P = &geo;
       const int64_t lo = phx_boundary(P, shard, nshards), hi = phx_boundary(P, shard + 1, nshards);
       if (word_range) {
         word_range[0] = phx_boundary_elem(P, lo);

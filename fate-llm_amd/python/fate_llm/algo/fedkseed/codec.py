@@ -186,7 +186,7 @@ def directional_step(specs: Sequence[ParamSpec], seeds: Sequence[int], values: S
     v = np.ascontiguousarray([float(x) for x in values], dtype=np.float64)
     with torch.cuda.device(b.device):
         if cache_windows and b.stream_mode == "torch_cpu":
-            jwin_reserve(b, len(s))
+            jwin_reserve(b, len(s), shard, nshards)
         ws, nbytes = b.workspace(len(s))
         N.check(L.fks_directional_step_shard(ctypes.addressof(b.arr), b.n, s.ctypes.data, v.ctypes.data, len(s),
                                              N.VALUE_TENSOR if value_is_tensor else N.VALUE_SCALAR,
@@ -261,23 +261,30 @@ def zindex_release(device=None) -> None:
 # fks.h, fks_jwin_attach): a client reconstructs the same seed list from model_0 every
 # round, so from the second round on the jumps are skipped.  A torch tensor taken under
 # JWIN_BUDGET_FRAC of the device's memory and never past its free memory (less
-# ZINDEX_HEADROOM); an allocation failure only means "jump"; FKS_NO_JWIN=1 turns it off.
+# ZINDEX_HEADROOM); an allocation failure only means "jump"; FKS_NO_JWIN=1 (or true / yes)
+# turns it off, as FKS_NO_JWIN does in the library (fks_capi.cpp env_on).
 JWIN_BUDGET_FRAC = float(os.environ.get("FKS_JWIN_BUDGET_FRAC", "0.05"))
 _jwin = {}  # device index -> attached uint8 tensor
+
+
+def _env_on(name: str) -> bool:
+    """A boolean switch: set to 1 / true / yes (any case); unset, empty, 0, false, no: off."""
+    return os.environ.get(name, "").strip().lower() in ("1", "true", "yes", "on")
 
 
 def _alloc_jwin(nbytes: int, device) -> torch.Tensor:
     return torch.empty(nbytes, dtype=torch.uint8, device=device)
 
 
-def jwin_reserve(b: "_Batch", k: int) -> bool:
+def jwin_reserve(b: "_Batch", k: int, shard: int = 0, nshards: int = 1) -> bool:
     """Attach a window cache that holds ``k`` seeds' window sets for the tensor list of
-    ``b`` on its device, if the budget allows; returns whether one is attached."""
-    if os.environ.get("FKS_NO_JWIN") or JWIN_BUDGET_FRAC <= 0:
+    ``b`` (element shard ``shard`` of ``nshards``: sets sized from that shard's plan) on
+    its device, if the budget allows; returns whether one is attached."""
+    if _env_on("FKS_NO_JWIN") or JWIN_BUDGET_FRAC <= 0:
         return False
     L = N.load()
     need = ctypes.c_size_t(0)
-    N.check(L.fks_jwin_size(ctypes.addressof(b.arr), b.n, int(k), ctypes.byref(need)))
+    N.check(L.fks_jwin_size_shard(ctypes.addressof(b.arr), b.n, int(k), int(shard), int(nshards), ctypes.byref(need)))
     need = int(need.value)
     if need == 0:
         return False

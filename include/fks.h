@@ -115,11 +115,15 @@ int fks_directional_step_shard(const fks_tensor* t, int32_t nt, const uint64_t* 
  * its model from model_0 and the same seed candidates every round
  * (python/fate_llm/algo/fedkseed/fedkseed.py:57-68, :132-141), so from the second round
  * on the reconstruct jumps nothing.  fks_jwin_size: bytes that hold k seeds' sets for
- * this tensor list (0: the call would not use the cache); fks_jwin_attach: attach `buf`
+ * this tensor list (0: the call would not use the cache); fks_jwin_size_shard: the same
+ * for the element shard `shard` of `nshards` (fks_directional_step_shard), sized from
+ * that shard's own plan -- an N-way shard's sets are about 1/N of the whole list's;
+ * fks_jwin_attach: attach `buf`
  * (bytes; NULL / 0 detaches), waiting for the last call that used the previous buffer;
  * fks_jwin_stats: seeds found / jumped since the library loaded.  Calls on any stream
  * are ordered by an event; fks_plan_cache_clear drops the contents. */
 int fks_jwin_size(const fks_tensor* t, int32_t nt, int32_t k, size_t* bytes);
+int fks_jwin_size_shard(const fks_tensor* t, int32_t nt, int32_t k, int32_t shard, int32_t nshards, size_t* bytes);
 int fks_jwin_attach(void* buf, size_t bytes);
 int fks_jwin_stats(uint64_t* hits, uint64_t* misses);
 

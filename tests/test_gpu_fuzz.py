@@ -4,7 +4,13 @@ to 2^17, with every dtype, mixed in one call), random per-tensor lr / weight dec
 +0.0, -0.0, 0.01, 0.3), K in 1..80 (the small-K kernel, the 19-seed fp32 and the 32/64-seed
 bf16 slice passes with their remainders), seeds past 2^32, scalars with zeros and edge
 values, applied whole or as 2 or 3 element shards, with the reconstruct window cache on
-or off.  Bit-exact (NaN matches NaN) against oracle.fks_oracle.reconstruct of the whole."""
+or off.  Bit-exact (NaN matches NaN) against oracle.fks_oracle.reconstruct of the whole.
+With the window cache on, the same call runs twice, cold then warm on a fresh copy of the
+parameters (a client's next round), half the time with a seed repeated inside the first
+64-seed pass: both results must match the oracle, and where the call uses the cache
+(fks_jwin_size_shard > 0) the warm call must find seeds in it."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -56,6 +62,8 @@ def _config(rng):
             vals[i] = float(rng.choice([1e-40, -3e38, 1e30, -0.0]))
     nshards = int(rng.choice([1, 1, 2, 3]))
     jwin = bool(rng.random() < 0.5)
+    if jwin and k >= 2 and rng.random() < 0.5:  # a seed twice inside one 64-seed pass
+        seeds[int(rng.integers(1, min(k, 64)))] = seeds[0]
     return sizes, dtypes, lrs, wds, seeds, vals, nshards, jwin
 
 
@@ -65,25 +73,40 @@ def test_random_call_matches_oracle(case):
     dev = _dev()
     rng = np.random.default_rng(1000 + case)
     sizes, dtypes, lrs, wds, seeds, vals, nshards, jwin = _config(rng)
+    from fate_llm.algo.fedkseed import _native as N
     g = torch.Generator().manual_seed(case)
     base = [to_np((torch.randn(n, generator=g) * 0.02).to(TD[d])) for n, d in zip(sizes, dtypes)]
-    ts = [from_np(a, d, dev) for a, d in zip(base, dtypes)]
-    specs = [codec.ParamSpec(t, lr=lr, weight_decay=wd) for t, lr, wd in zip(ts, lrs, wds)]
     # train_once drops g == 0.0 entries (fedkseed.py:137; zo_utils.reconstruct_), the oracle too
     ks = [s for s, v in zip(seeds, vals) if v != 0.0]
     kv = [v for v in vals if v != 0.0]
-    if ks:
-        if nshards == 1:
-            codec.directional_step(specs, ks, kv, cache_windows=jwin)
-        else:
-            for r in range(nshards):
-                codec.directional_step(specs, ks, kv, shard=r, nshards=nshards, cache_windows=jwin)
-    torch.cuda.synchronize()
     ref = [a.copy() for a in base]
     O.reconstruct(ref, [DTC[d] for d in dtypes], lrs, wds, seeds, vals)
     what = f"case {case}: sizes {sizes} dtypes {dtypes} wds {wds} k {len(seeds)} shards {nshards} jwin {jwin}"
-    for t, r_, d in zip(ts, ref, dtypes):
-        assert_bitwise(to_np(t), r_, d, what)
+
+    def run(label):
+        ts = [from_np(a, d, dev) for a, d in zip(base, dtypes)]
+        specs = [codec.ParamSpec(t, lr=lr, weight_decay=wd) for t, lr, wd in zip(ts, lrs, wds)]
+        if ks:
+            for r in range(nshards):
+                codec.directional_step(specs, ks, kv, shard=r, nshards=nshards, cache_windows=jwin)
+        torch.cuda.synchronize()
+        for t, r_, d in zip(ts, ref, dtypes):
+            assert_bitwise(to_np(t), r_, d, f"{what} ({label})")
+        return specs
+
+    specs = run("cold")
+    if jwin and ks:
+        used = False  # does any shard's call use the window cache?
+        b = codec._Batch(specs)
+        for r in range(nshards):
+            need = ctypes.c_size_t(0)
+            N.check(N.load().fks_jwin_size_shard(ctypes.addressof(b.arr), b.n, len(ks), r, nshards, ctypes.byref(need)))
+            used |= need.value > 0
+        hits0, _ = codec.jwin_stats()
+        run("warm")
+        hits1, _ = codec.jwin_stats()
+        if used:
+            assert hits1 > hits0, f"{what}: the warm call found no seed in the window cache"
 
 
 def _rocm_reference(params, seeds, vals, lrs, wds):

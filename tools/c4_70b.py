@@ -15,6 +15,17 @@ count (linearity checked on two sample sizes).  Prints one JSON line.
 --check K (needs room for a second copy of the buffer, e.g. --scale 0.4): before timing,
 reconstruct K seeds chunked and, on a clone, in one unchunked call, and report whether
 the two agree bit for bit (tests/test_gpu_c4.py holds the oracle comparison).
+
+--verify OUT.npz (full size, with --ks 4096): checks of the 276 GB result itself, around
+the timed run (zo_utils.py:47-49 over 723 tensors, fedkseed.py:136-141):
+  * the first 4096 elements of embed_tokens before and after the whole reconstruct, with
+    the seeds and scalars, are written to OUT.npz; tests/test_c4_fullsize_record.py
+    replays them through the oracle (tools/ does not run the oracle);
+  * a chunk boundary recomputed by ONE call: the elements within --window of the boundary
+    between chunks C/2 - 1 and C/2 (computed by two calls in the timed run) are saved,
+    reset to their initial values and reconstructed again by a single element-shard call
+    whose shard holds the boundary in its interior (the rest of that shard is updated a
+    second time, which the check ignores); the window must come back bit for bit.
 """
 import argparse
 import json
@@ -50,6 +61,8 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0, help="fraction of every tensor's rows (smoke runs)")
     ap.add_argument("--progress", action="store_true", help="one stderr line per chunk (long runs)")
     ap.add_argument("--check", type=int, default=0, help="K seeds: chunked vs unchunked, bit for bit")
+    ap.add_argument("--verify", default="", help="OUT.npz: full-size checks of the reconstructed buffer")
+    ap.add_argument("--window", type=int, default=1 << 24, help="--verify: elements on each side of the boundary")
     args = ap.parse_args()
     from fate_llm.algo.fedkseed import codec
 
@@ -97,6 +110,15 @@ def main():
     for c in range(args.chunks):
         codec.directional_step(specs, [keep[0][0]], [keep[0][1]], shard=c, nshards=args.chunks)
     torch.cuda.synchronize()
+    if args.verify:
+        if len(args.ks.split(",")) != 1:
+            raise SystemExit("--verify times one sample: give --ks a single K (4096 for the full run)")
+        # the values the timed run starts from (the warm-up seed above is one more step of
+        # the same stream: the oracle replay starts after it as well)
+        emb0 = flat[:4096].cpu().numpy().copy()
+        bnd = codec.shard_range(specs, args.chunks // 2, args.chunks)[0]  # first element of chunk C/2
+        lo, hi = max(0, bnd - args.window), min(total, bnd + args.window)
+        win0 = flat[lo:hi].cpu()
 
     samples = []
     for k in [int(x) for x in args.ks.split(",")]:
@@ -117,6 +139,39 @@ def main():
                         "apply_ms_per_launch": round(prof.apply_ms / max(prof.n_apply, 1), 3),
                         "launches": prof.n_apply, "jump_ms": round(prof.jump_ms, 1)})
         print(json.dumps(samples[-1]), flush=True)
+    verify = None
+    if args.verify:
+        ks, kv = [s for s, _ in keep[:samples[-1]["k"]]], [g for _, g in keep[:samples[-1]["k"]]]
+        emb1 = flat[:4096].cpu().numpy().copy()
+        win1 = flat[lo:hi].cpu()
+        # the single call: the element shard of an N-way split that holds [lo, hi) inside
+        one = None
+        for n in range(3, 64):
+            for r in range(n):
+                a, b = codec.shard_range(specs, r, n)
+                if a < lo and hi < b:
+                    one = (r, n, a, b)
+                    break
+            if one:
+                break
+        flat[lo:hi].copy_(win0.to(dev))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        codec.directional_step(specs, ks, kv, shard=one[0], nshards=one[1])
+        torch.cuda.synchronize()
+        t_one = time.perf_counter() - t0
+        win2 = flat[lo:hi].cpu()
+        differ = int((win1.view(torch.int32) != win2.view(torch.int32)).sum().item())
+        import numpy as np
+        np.savez_compressed(args.verify, embed_before=emb0, embed_after=emb1,
+                            seeds=np.asarray(ks, dtype=np.uint64), scalars=np.asarray(kv, dtype=np.float64),
+                            lr=np.float64(1e-5), weight_decay=np.float64(0.01), params=np.int64(total))
+        verify = {"embed_prefix_file": os.path.basename(args.verify), "boundary_element": bnd,
+                  "window": [lo, hi], "single_call_shard": [one[0], one[1]], "single_call_elements": [one[2], one[3]],
+                  "single_call_s": round(t_one, 2), "window_elements_differing": differ,
+                  "boundary_bit_identical": differ == 0,
+                  "changed_by_reconstruct": int((win1.view(torch.int32) != win0.view(torch.int32)).sum().item())}
+        print(json.dumps({"verify": verify}), flush=True)
     per_pass = samples[-1]["s_per_pass"]
     t_full = per_pass * passes_full
     out = {
@@ -129,8 +184,10 @@ def main():
         "seed_param_per_s": round(total * 19 / per_pass, 1),
         "data": "synthetic: random-init N(0, 0.02^2) fp32, seeds/scalars of bench.synthetic_seeds(4096)",
     }
+    if verify is not None:
+        out["verify"] = verify
     print(json.dumps(out), flush=True)
-    return 0
+    return 0 if verify is None or verify["boundary_bit_identical"] else 3
 
 
 if __name__ == "__main__":
