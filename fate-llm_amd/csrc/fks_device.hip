@@ -34,6 +34,15 @@ constexpr int kDbMinWaves = 4;   // launch-bounds waves per SIMD of the double-b
 constexpr int kZrUnroll = 2;     // z-index replay: tiles per loop iteration (in flight per wave)
 constexpr int kSm2MinWaves = 8;  // launch-bounds waves per SIMD of fks_small2_kernel (8 workgroups of 4 waves per CU: <= 64 VGPRs)
 constexpr int kBsFence = 8;      // slice kernel: compiler fence after every 8 seeds' table lookups
+#ifndef FKS_BS_LAG               // slice kernel, two-slice passes: half 0 twists task n only once half 1
+#define FKS_BS_LAG 36            // has applied task n - FKS_BS_LAG (0: unbounded; must exceed 12)
+#endif
+#ifndef FKS_F32_SEED_PAIRS       // fp32 19-seed kernel: seed PAIRS sharing packed float ops, this many
+#define FKS_F32_SEED_PAIRS 0     // interleaved per step (0: one seed per z computation).  Measured
+#endif                           // 7-9 % SLOWER for 1-3 (profiles/r05c_f32_seedpair_ab.log)
+#ifndef FKS_LOG_INTMASK          // fp32 Cephes log: the x < sqrt(1/2) select as integer arithmetic
+#define FKS_LOG_INTMASK 1
+#endif
 
 namespace fks {
 namespace {
@@ -86,6 +95,18 @@ __device__ __forceinline__ uint32_t swap_adjacent(uint32_t v) {
 // contractions GCC applies in libtorch's AVX2/AVX512 build (pinned bit-exact by
 // oracle/fks_oracle.c against the reference's golden streams).
 __device__ __forceinline__ float cephes_logf(float x) {  // x in [2^-24, 1]
+#if FKS_LOG_INTMASK
+  // the "x < sqrt(1/2)" select as integer arithmetic: x is a normal float in [0.5, 1)
+  // (ordered like its bits), the mask the sign of bits(x) - bits(0.70710678f); "mask ? x :
+  // 0" is bits(x) & mask and e = float(imm0 - 126 + mask) the exact integer
+  // (imm0 - 0x7f) + 1 - (mask ? 1 : 0): no compare, no select, no hazard wait
+  const uint32_t xb0 = __float_as_uint(x);
+  const uint32_t xb = (xb0 & ~0x7f800000u) | 0x3f000000u;
+  const int32_t m = (int32_t)(xb - 0x3F3504F3u) >> 31;
+  const float e = (float)((int32_t)(xb0 >> 23) - 126 + m);
+  const float tmp = __uint_as_float(xb & (uint32_t)m);
+  x = __uint_as_float(xb) - 1.0f;
+#else
   int32_t imm0 = (int32_t)(__float_as_uint(x) >> 23);
   x = __uint_as_float((__float_as_uint(x) & ~0x7f800000u) | 0x3f000000u);
   imm0 -= 0x7f;
@@ -95,6 +116,7 @@ __device__ __forceinline__ float cephes_logf(float x) {  // x in [2^-24, 1]
   const float tmp = mask ? x : 0.0f;
   x = x - 1.0f;
   e = e - (mask ? 1.0f : 0.0f);
+#endif
   x = x + tmp;
   const float z = x * x;
   float y = 7.0376836292E-2f;
@@ -924,6 +946,158 @@ __device__ __forceinline__ void z_pair_f32_raw(uint32_t r1, uint32_t r2, float& 
   z2 = __fmaf_rn(radius, s, 0.0f);
 }
 
+// The same z pairs for TWO seeds at once (the fp32 19-seed kernel's full passes): every
+// float operation of cephes_logf / the radius / cephes_sincosf_nonneg runs on the two
+// seeds' values as one packed f32 instruction (v_pk_mul/add/fma_f32: per element the same
+// IEEE operation, so the same bits); the integer work stays per seed.  cephes_logf's
+// "x < sqrt(1/2)" select becomes integer arithmetic on the bits -- the mask is the sign of
+// bits(x) - bits(0.70710678f) (x is a normal float in [0.5, 1): ordered like its bits);
+// "mask ? x : 0" is bits(x) & mask and e = float(imm0 - 126 + mask) is the exact integer
+// e + 1 - (mask ? 1 : 0) -- no compare, no select, no hazard wait.
+__device__ __forceinline__ f32x2_t pk(float a, float b) { return (f32x2_t){a, b}; }
+__device__ __forceinline__ f32x2_t pk1(float a) { return (f32x2_t){a, a}; }
+// Q packed pairs side by side, every step issued for all Q before the next: a dependent
+// v_pk_*_f32 right after its producer costs a wait state on gfx950, so the Horner chains
+// of the Q pairs are interleaved in the source (each step's Q ops are independent).
+#define FKS_Q for (int q = 0; q < Q; q++)
+template <int Q>
+__device__ __forceinline__ void cephes_logf2(f32x2_t (&x)[Q]) {  // every value in [2^-24, 1]
+  f32x2_t e[Q], z[Q], y[Q], tm[Q];
+#pragma unroll
+  FKS_Q {
+    float xm[2], tmv[2], ef[2];
+    const uint32_t b[2] = {__float_as_uint(x[q].x), __float_as_uint(x[q].y)};
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const uint32_t xb = (b[i] & ~0x7f800000u) | 0x3f000000u;  // mantissa in [0.5, 1)
+      const int32_t m = (int32_t)(xb - 0x3F3504F3u) >> 31;      // -1 iff x < 0.707106781186547524f
+      xm[i] = __uint_as_float(xb);
+      tmv[i] = __uint_as_float(xb & (uint32_t)m);               // mask ? x : 0
+      ef[i] = (float)((int32_t)(b[i] >> 23) - 126 + m);         // (imm0 - 0x7f) + 1 - (mask ? 1 : 0)
+    }
+    x[q] = pk(xm[0], xm[1]);
+    tm[q] = pk(tmv[0], tmv[1]);
+    e[q] = pk(ef[0], ef[1]);
+  }
+#pragma unroll
+  FKS_Q x[q] = x[q] - pk1(1.0f);
+#pragma unroll
+  FKS_Q x[q] = x[q] + tm[q];
+#pragma unroll
+  FKS_Q z[q] = x[q] * x[q];
+#pragma unroll
+  FKS_Q y[q] = __builtin_elementwise_fma(pk1(7.0376836292E-2f), x[q], pk1(-1.1514610310E-1f));
+  constexpr float kC[7] = {1.1676998740E-1f, -1.2420140846E-1f, +1.4249322787E-1f, -1.6668057665E-1f,
+                           +2.0000714765E-1f, -2.4999993993E-1f, +3.3333331174E-1f};
+#pragma unroll
+  for (int t = 0; t < 7; t++) {
+#pragma unroll
+    FKS_Q y[q] = __builtin_elementwise_fma(y[q], x[q], pk1(kC[t]));
+  }
+#pragma unroll
+  FKS_Q y[q] = y[q] * x[q];
+#pragma unroll
+  FKS_Q y[q] = __builtin_elementwise_fma(y[q], z[q], e[q] * pk1(-2.12194440e-4f));
+#pragma unroll
+  FKS_Q y[q] = __builtin_elementwise_fma(-z[q], pk1(0.5f), y[q]);
+#pragma unroll
+  FKS_Q x[q] = x[q] + y[q];
+#pragma unroll
+  FKS_Q x[q] = __builtin_elementwise_fma(e[q], pk1(0.693359375f), x[q]);
+}
+
+template <int Q>
+__device__ __forceinline__ void cephes_sincosf2_nonneg(f32x2_t (&x)[Q], f32x2_t (&s)[Q], f32x2_t (&c)[Q]) {
+  f32x2_t y[Q], z[Q], yc[Q], ys[Q];
+  int32_t imm2[Q][2];
+#pragma unroll
+  FKS_Q y[q] = x[q] * pk1(1.27323954473516f);
+#pragma unroll
+  FKS_Q {
+    imm2[q][0] = ((int32_t)y[q].x + 1) & ~1;
+    imm2[q][1] = ((int32_t)y[q].y + 1) & ~1;
+    y[q] = pk((float)imm2[q][0], (float)imm2[q][1]);
+  }
+#pragma unroll
+  FKS_Q x[q] = __builtin_elementwise_fma(y[q], pk1(-0.78515625f), x[q]);
+#pragma unroll
+  FKS_Q x[q] = __builtin_elementwise_fma(y[q], pk1(-2.4187564849853515625e-4f), x[q]);
+#pragma unroll
+  FKS_Q x[q] = __builtin_elementwise_fma(y[q], pk1(-3.77489497744594108e-8f), x[q]);
+#pragma unroll
+  FKS_Q z[q] = x[q] * x[q];
+#pragma unroll
+  FKS_Q {
+    yc[q] = __builtin_elementwise_fma(pk1(2.443315711809948E-005f), z[q], pk1(-1.388731625493765E-003f));
+    ys[q] = __builtin_elementwise_fma(pk1(-1.9515295891E-4f), z[q], pk1(8.3321608736E-3f));
+  }
+#pragma unroll
+  FKS_Q {
+    yc[q] = __builtin_elementwise_fma(yc[q], z[q], pk1(4.166664568298827E-002f));
+    ys[q] = __builtin_elementwise_fma(ys[q], z[q], pk1(-1.6666654611E-1f));
+  }
+#pragma unroll
+  FKS_Q {
+    yc[q] = yc[q] * z[q];
+    ys[q] = ys[q] * z[q];
+  }
+#pragma unroll
+  FKS_Q {
+    yc[q] = __builtin_elementwise_fma(yc[q], z[q], -(z[q] * pk1(0.5f)));
+    ys[q] = __builtin_elementwise_fma(ys[q], x[q], x[q]);
+  }
+#pragma unroll
+  FKS_Q yc[q] = yc[q] + pk1(1.0f);
+#pragma unroll
+  FKS_Q {
+    float so[2], co[2];
+    const float ysv[2] = {ys[q].x, ys[q].y}, ycv[2] = {yc[q].x, yc[q].y};
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const uint32_t sign_bit_sin = ((uint32_t)(imm2[q][i] & 4)) << 29;
+      const uint32_t sign_bit_cos = ((uint32_t)(~(imm2[q][i] - 2) & 4)) << 29;
+      const bool poly_mask = (imm2[q][i] & 2) == 0;
+      so[i] = __uint_as_float(__float_as_uint(poly_mask ? ysv[i] : ycv[i]) ^ sign_bit_sin);
+      co[i] = __uint_as_float(__float_as_uint(poly_mask ? ycv[i] : ysv[i]) ^ sign_bit_cos);
+    }
+    s[q] = pk(so[0], so[1]);
+    c[q] = pk(co[0], co[1]);
+  }
+}
+
+// z pairs (z_j, z_{j+8}) of 2Q seeds from their raw word pairs w[0..2Q) (as
+// z_pair_f32_raw; seeds 2q and 2q+1 share packed float instructions)
+template <int Q>
+__device__ __forceinline__ void z_pair_f32x2_raw(const u32x2_t (&w)[2 * Q], f32x2_t (&zo)[2 * Q]) {
+  f32x2_t d1[Q], d2[Q], v[Q], s[Q], c[Q];
+#pragma unroll
+  FKS_Q {
+    const u32x2_t ta = temper_pair_u24(w[2 * q]), tb = temper_pair_u24(w[2 * q + 1]);
+    d1[q] = pk((float)ta.x, (float)tb.x) * pk1(1.0f / 16777216.0f);
+    d2[q] = pk((float)ta.y, (float)tb.y) * pk1(1.0f / 16777216.0f);
+  }
+#pragma unroll
+  FKS_Q v[q] = pk1(1.0f) - d1[q];
+  cephes_logf2<Q>(v);
+#pragma unroll
+  FKS_Q v[q] = pk1(-2.0f) * v[q];
+  float r[2 * Q];
+#pragma unroll
+  FKS_Q {
+    r[2 * q] = radius_sqrt(v[q].x);
+    r[2 * q + 1] = radius_sqrt(v[q].y);
+  }
+#pragma unroll
+  FKS_Q v[q] = pk1(6.28318548202514648438f) * d2[q];
+  cephes_sincosf2_nonneg<Q>(v, s, c);
+#pragma unroll
+  FKS_Q {
+    zo[2 * q] = __builtin_elementwise_fma(pk1(r[2 * q]), pk(c[q].x, s[q].x), pk1(0.0f));
+    zo[2 * q + 1] = __builtin_elementwise_fma(pk1(r[2 * q + 1]), pk(c[q].y, s[q].y), pk1(0.0f));
+  }
+}
+#undef FKS_Q
+
 // bf16 Box-Muller pair before the final rounding: (R[a] * C[b], R[a] * S[b]) + 0 as ONE
 // v_pk_fma_f32 (R*C is exact in f32: 8-bit x 8-bit significands; the +0 addend turns
 // -0 into +0 like normal_fill_16's "+ mean").  (R,R) pairs at LDS 0, (C,S) pairs at 2048.
@@ -1034,8 +1208,24 @@ __device__ __forceinline__ void pair_all(const uint8_t* lds, int st_off, const f
     r2[k] = (uint32_t)(w >> 32);
   }
   f32x2_t z[NS];
+  if constexpr (DT == FKS_F32 && FKS_F32_SEED_PAIRS > 0) {  // seed pairs share packed float ops
+    constexpr int Q = FKS_F32_SEED_PAIRS > 0 ? FKS_F32_SEED_PAIRS : 1;  // pairs interleaved per step
 #pragma unroll
-  for (int k = 0; k < NS; k++) z[k] = z_pair2<DT>(lds, r1[k], r2[k]);
+    for (int k = 0; k + 2 * Q <= NS; k += 2 * Q) {
+      u32x2_t w[2 * Q];
+      f32x2_t zz[2 * Q];
+#pragma unroll
+      for (int i = 0; i < 2 * Q; i++) w[i] = (u32x2_t){r1[k + i], r2[k + i]};
+      z_pair_f32x2_raw<Q>(w, zz);
+#pragma unroll
+      for (int i = 0; i < 2 * Q; i++) z[k + i] = zz[i];
+    }
+#pragma unroll
+    for (int k = NS - NS % (2 * Q); k < NS; k++) z[k] = z_pair2<DT>(lds, r1[k], r2[k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < NS; k++) z[k] = z_pair2<DT>(lds, r1[k], r2[k]);
+  }
   f32x2_t p = {p1, p2};
 #pragma unroll
   for (int k = 0; k < NS; k++) p = apply_pair<DT, MODE>(p, z[k], g[k], lr, wd, has_wd, ps);
@@ -1699,7 +1889,8 @@ constexpr int kBsStateBytes = 8 * kBsChunkBytes;       // 79,872
 constexpr int kBsTabBytes = 256 * 4 + 256 * 8;         // 3,072
 constexpr uint32_t kBsFlagOff = kBsTabBytes + 2 * kBsStateBytes;  // u32 twisted-task count per half
 constexpr uint32_t kBsProgOff = kBsFlagOff + 8;        // u32 per half-0 wave: its tasks < value are stored
-constexpr int kBsLdsBytes = (int)kBsProgOff + 4 * 6;   // 162,848 <= 163,840
+constexpr uint32_t kBsProg1Off = kBsProgOff + 4 * 6;   // u32 per half-1 wave: its tasks < value are done
+constexpr int kBsLdsBytes = (int)kBsProg1Off + 4 * 6;  // 162,872 <= 163,840
 static_assert(kBsLdsBytes <= 163840, "slice kernel LDS");
 constexpr int kBsWaves = kBsHalfThreads / 64;          // waves per half (6)
 constexpr int kBsTaskWords = 128;                      // stream words per task
@@ -1791,7 +1982,7 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
     bs_store_row(sbase + 16u * (uint32_t)i, w);
   }
   if (ht == 0) lds32[flag / 4] = 0u;
-  if (half == 0 && ht < kBsWaves) lds32[kBsProgOff / 4 + ht] = 0u;
+  if (ht < kBsWaves) lds32[(half ? kBsProg1Off : kBsProgOff) / 4 + ht] = 0u;
   __syncthreads();  // the only workgroup barrier
   if (nseeds == 0) return;  // a one-seed pass: slice 1 is empty
 
@@ -1981,11 +2172,28 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
     while (__builtin_amdgcn_readfirstlane(bs_flag_load(pm)) < (uint32_t)m + 1u) __builtin_amdgcn_s_sleep(1);
     asm volatile("" ::: "memory");
   };
+  // The lag bound.  Nothing else keeps half 0 from running ahead of half 1 (it wins the
+  // VALU arbitration by age), and with the longer weight-decay chain half 1 fell so far
+  // behind that its loads of half 0's output came back from HBM (7.9 B/param per launch,
+  // profiles/pmc_apply_r04_full.json).  Half 1 publishes each task as applied; half 0 waits
+  // for task n - FKS_BS_LAG before twisting task n.  Half 1's task m needs half 0's task
+  // m + 2 kBsWaves (publish_stored), so the bound must exceed 2 kBsWaves = 12.
+  static_assert(FKS_BS_LAG == 0 || FKS_BS_LAG > 2 * kBsWaves, "FKS_BS_LAG: half 1 trails by 12 tasks");
+  const uint32_t prog1 = kBsProg1Off + 4u * (uint32_t)hw;
+  auto publish_applied = [&](const int m) {
+    if (lane == 0) *(volatile lds_u32_t*)(size_t)prog1 = (uint32_t)m + 1u;
+  };
+  auto await_applied = [&](const int m) {
+    if (m < 0) return;
+    const uint32_t pm = kBsProg1Off + 4u * (uint32_t)(m % kBsWaves);
+    while (__builtin_amdgcn_readfirstlane(bs_flag_load(pm)) < (uint32_t)m + 1u) __builtin_amdgcn_s_sleep(1);
+  };
 
   // ---- task n: wait for task n-1's twist, twist, publish, chain; fetches task n + 6
   // into nx (past the last task: the sink)
   auto task = [&](const int n, const Slot& sl, Slot& nx) {
     uint32_t oa[8], ob[8];
+    if (FKS_BS_LAG > 0 && ordered && half == 0) await_applied(n - FKS_BS_LAG);
     __builtin_amdgcn_s_setprio(2);
 #if !FKS_BS_DIAG_NOWAIT  // diagnostic (wrong values): no hand-off wait, the resource bound
     while (__builtin_amdgcn_readfirstlane(bs_flag_load(flag)) < (uint32_t)n) __builtin_amdgcn_s_sleep(0);
@@ -2005,6 +2213,7 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
 #else
     chain(sl, oa, ob);
 #endif
+    if (FKS_BS_LAG > 0 && ordered && half) publish_applied(n);
   };
 
   // two named slots and a loop unrolled by two: a slot copy on the back edge would wait

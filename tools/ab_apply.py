@@ -37,7 +37,7 @@ print(json.dumps({"lib": os.environ.get("FKS_LIB_OVERRIDE", "libfks.so"), "dtype
 
 
 def main():
-    libs = sys.argv[1:] or [""]
+    libs = [("" if a == "intree" else a) for a in sys.argv[1:]] or [""]  # "intree": the in-tree libfks.so
     for lib in libs:
         env = dict(os.environ, ROOT=ROOT, AB_N=os.environ.get("AB_N", str(1 << 28)),
                    AB_K=os.environ.get("AB_K", "95"))

@@ -63,7 +63,7 @@ for step in "$@"; do
     sh)
       timeout -k 10 1200 bash "tools/$arg" > "$log" 2>&1 ;;
     ab)
-      timeout -k 10 600 python -u tools/ab_apply.py $(echo "$arg" | tr ',' ' ' | sed -e 's#intree##g') > "$log" 2>&1 ;;
+      timeout -k 10 600 python -u tools/ab_apply.py $(echo "$arg" | tr ',' ' ') > "$log" 2>&1 ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
