@@ -730,6 +730,8 @@ struct PhxPlan {
   int nt = 0;           // table entries (tensors with work items)
   int64_t items = 0;    // work items of all tensors
   int wd_mode = kModeUpdate;  // kModeUpdateWd / NoWd / Wd0 when every tensor shares the form
+  bool wd_pos0 = false;        // Wd0 with wd = +0.0 on bf16 / f32 tensors only (kModeUpdateWdPos0 candidate)
+  float max_lr = 0.0f;         // max |lr| over the table (the WdPos0 bound)
   std::vector<PhxTensor> tab;  // host copy of the table
   std::vector<int64_t> elem0;  // per entry: its first element in the concatenation of ALL the call's tensors
   int64_t elems = 0;           // elements of all the call's tensors
@@ -1000,6 +1002,14 @@ void phx_geometry(const fks_tensor* t, int nt, const double* scales, PhxPlan* P)
     if (!tab.empty() && nwd0 == tab.size()) P->wd_mode = kModeUpdateWd0;
     else if (!tab.empty() && nwd == tab.size()) P->wd_mode = kModeUpdateWd;
     else if (!tab.empty() && nwd == 0) P->wd_mode = kModeUpdateNoWd;
+    bool pos0 = P->wd_mode == kModeUpdateWd0;
+    for (const PhxTensor& x : tab) {
+      uint32_t wb;
+      std::memcpy(&wb, &x.wd, 4);
+      pos0 = pos0 && wb == 0u && x.dtype != FKS_F16 && std::isfinite(x.lr);
+      P->max_lr = std::max(P->max_lr, std::fabs(x.lr));
+    }
+    P->wd_pos0 = pos0;
   }
   P->tab = std::move(tab);
   P->elem0 = std::move(elem0);
@@ -1093,6 +1103,19 @@ void run_philox(const fks_tensor* t, int nt, const uint64_t* seeds, const double
   a.item_lo = phx_boundary(P, shard, nshards);
   a.item_hi = phx_boundary(P, shard + 1, nshards);
   if (a.item_lo >= a.item_hi) return;
+  if (a.mode == kModeUpdateWd0 && P->wd_pos0 && !env_on("FKS_PHX_KEEP_WD_FMA")) {
+    // kModeUpdateWdPos0 when |lr g z| stays <= 1e30 for every seed (|z| <= 6.67: the
+    // largest Box-Muller radius is sqrt(-2 ln 2^-32) = 6.66): no overflow, so t = gz
+    double gmax = 0.0;
+    bool finite = std::isfinite((double)P->max_lr);
+    for (int j = 0; j < k && finite; j++)
+      for (int d = 0; d < 2; d++) {  // FKS_F32, FKS_BF16: the g the kernels see
+        const float g = value_kind == FKS_VALUE_TENSOR ? round_to_dtype(values[j], d) : (float)values[j];
+        finite = finite && std::isfinite(g);
+        gmax = std::max(gmax, (double)std::fabs(g));
+      }
+    if (finite && gmax * 6.67 <= 1e37 && gmax * 6.67 * (double)P->max_lr <= 1e30) a.mode = kModeUpdateWdPos0;
+  }
   for (int s0 = 0; s0 < k; s0 += kPhxSeeds) {
     const int nb = std::min(kPhxSeeds, k - s0);
     for (int j = 0; j < nb; j++) {

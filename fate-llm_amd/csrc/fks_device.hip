@@ -1144,7 +1144,7 @@ __device__ __forceinline__ f32x2_t rnd2(f32x2_t x) {
 template <int DT, int MODE>
 __device__ __forceinline__ f32x2_t apply_tail(f32x2_t p, f32x2_t gz, float lr, float wd, bool has_wd) {
   f32x2_t t;
-  if (MODE == kModeUpdateNoWd) {
+  if (MODE == kModeUpdateNoWd || MODE == kModeUpdateWdPos0) {
     t = gz;
   } else if (MODE == kModeUpdateWd0) {
     // wd = +-0: rnd(gz + rnd(wd*p)) == fma(wd, p, gz) (fks_internal.h)
@@ -1174,7 +1174,7 @@ __device__ __forceinline__ f32x2_t apply_pair(f32x2_t p, f32x2_t z, float g, flo
     if (MODE == kModePerturb || !upd) return p;
   }
   if (MODE == kModeUpdate || MODE == kModeUpdateWd || MODE == kModeUpdateNoWd || MODE == kModePerturbUpdate ||
-      MODE == kModeUpdateWd0)
+      MODE == kModeUpdateWd0 || MODE == kModeUpdateWdPos0)
     return apply_tail<DT, MODE>(p, rnd2<DT>(g * z), lr, wd, has_wd);
   return z;
 }
@@ -2579,8 +2579,10 @@ __device__ __forceinline__ float phx_radius_ocml(uint32_t x) {
 // The item's four elements through every seed of the pass, in seed order, as two packed
 // pairs (apply_pair: the values of apply_one); MODE may be a launch-wide weight-decay
 // specialisation of kModeUpdate (kModeUpdateWd / NoWd / Wd0, as the CPU stream's kernels).
-template <int DT, int MODE>
+template <int DT, int MODE_>
 __device__ __forceinline__ void phx_item(const PhiloxArgs& a, const PhxTensor& T, int64_t r) {
+  // (the host gives kModeUpdateWdPos0 launches bf16 / f32 tensors only)
+  constexpr int MODE = (MODE_ == kModeUpdateWdPos0 && DT == FKS_F16) ? (int)kModeUpdateWd0 : MODE_;
   using TR = Traits<DT>;
   const uint32_t S = T.stride;
   const uint32_t idx = (uint32_t)(r % S);
@@ -2593,6 +2595,8 @@ __device__ __forceinline__ void phx_item(const PhiloxArgs& a, const PhxTensor& T
     e[i] = (int64_t)idx + (int64_t)S * (int64_t)(4 * j + i);
     on[i] = e[i] < T.numel;
     p[i] = (MODE != kModeWriteZ && on[i]) ? TR::load(T.ptr, e[i]) : 0.0f;
+    // kModeUpdateWdPos0: a +-inf parameter is NaN after the reference's first seed (wd * p)
+    if (MODE == kModeUpdateWdPos0 && __builtin_isinf(p[i])) p[i] = __builtin_nanf("");
   }
   const bool has_wd = (T.flags & FKS_HAS_WD) != 0;
   const bool dv = MODE == kModePerturbUpdate && a.gdev;
@@ -2955,6 +2959,7 @@ int launch_philox(const PhiloxArgs& a, void* stream) {
     case kModeUpdateWd: return launch_philox_m<kModeUpdateWd>(a, stream);
     case kModeUpdateNoWd: return launch_philox_m<kModeUpdateNoWd>(a, stream);
     case kModeUpdateWd0: return launch_philox_m<kModeUpdateWd0>(a, stream);
+    case kModeUpdateWdPos0: return launch_philox_m<kModeUpdateWdPos0>(a, stream);
     case kModePerturb: return launch_philox_m<kModePerturb>(a, stream);
     case kModePerturbUpdate: return launch_philox_m<kModePerturbUpdate>(a, stream);
     case kModeWriteZ: return launch_philox_m<kModeWriteZ>(a, stream);

@@ -107,6 +107,15 @@ constexpr int kJumpXLen = 19937 + 624;  // x[0..20560]: y[i + w] = x[i + w + 1],
 // exactly gz, +-0 or NaN, so both roundings are identities and t = fma(wd, p, gz) gives
 // the same bits (signed zeros and NaNs included) with one instruction instead of six
 // per element pair
+// kModeUpdateWdPos0 (torch_rocm stream only): every tensor has wd = +0.0 exactly, is bf16
+// or f32, and the host has bounded |lr g z| <= 1e30 for every seed of the call; then for a
+// finite p the fma above is exactly gz (wd*p is +0 for p >= +0, -0 for p <= -0, and the
+// only sum that differs from gz, -0 + +0 = +0, is followed by lr*t and p - that, whose
+// result for p >= +0 does not depend on that zero's sign), p - lr*t cannot overflow, and a
+// +-inf p -- which the reference turns into NaN at the first seed (0 * inf) -- is set to
+// NaN at load: t = gz, one packed op per element pair and seed fewer
+enum ApplyModeExt : int { kModeUpdateWdPos0 = 8 };
+
 // kModePerturbUpdate: p + ps*z, then the update with the same z (the restore
 // perturbation of zeroth_order_step fused with its directional step)
 // kModeDelta: the seed-sharded variant; z is accumulated into an f32 delta buffer,

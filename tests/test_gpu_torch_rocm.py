@@ -78,6 +78,48 @@ def test_reconstruct_matches_torch_on_device(dtype, wd):
         _assert_same(a, b, f"tensor {i}")
 
 
+@pytest.mark.parametrize("wd", [0.0, -0.0])
+@pytest.mark.parametrize("gscale", [20.0, 1e36])
+@pytest.mark.parametrize("keep_fma", [False, True])
+def test_zero_weight_decay_edge_values(wd, gscale, keep_fma, monkeypatch):
+    """wd = +-0 (the HF default the reference's ClientTrainer passes, fedkseed.py:140) with
+    zeros of both signs, +-inf, NaN, subnormals and huge values among the parameters, bf16
+    / f32 / f16 tensors in one call: wd = +0 on bf16 / f32 with a bounded |lr g z| takes
+    kModeUpdateWdPos0 (t = g z, an infinite parameter set to NaN at load), everything else
+    the fma chain; FKS_PHX_KEEP_WD_FMA=1 forces the fma chain.  Against the reference's
+    expression as torch ops on the device, bit for bit (NaN payloads aside)."""
+    from fate_llm.algo.fedkseed import codec
+    if keep_fma:
+        monkeypatch.setenv("FKS_PHX_KEEP_WD_FMA", "1")
+    dev = _dev()
+    edge = torch.tensor([0.0, -0.0, float("inf"), float("-inf"), float("nan"), 1e-40, -1e-42, 3e38, -3e38,
+                         1e-3, -2.5e-2, 65000.0, 1.0, -1.0, 1e-8, 7e-39], dtype=torch.float32)
+    base = []
+    for i, dt in enumerate(["bfloat16", "float32", "bfloat16", "float16"]):
+        g = torch.Generator().manual_seed(11 + i)
+        x = torch.randn(4096 + 517 * i, generator=g) * 0.02
+        x[: edge.numel()] = edge
+        x[1000:1000 + edge.numel()] = edge
+        base.append(x.to(DT[dt]).to(dev))
+    if wd == 0.0 and str(wd) == "0.0":  # +0: drop the f16 tensor so the launch can take WdPos0
+        base = base[:3] if not keep_fma else base
+    g = torch.Generator().manual_seed(3)
+    seeds = torch.randint(0, 2**32, (35,), generator=g).tolist()
+    vals = (torch.randn(35, generator=g, dtype=torch.float64) * gscale).tolist()
+    vals[4] = -vals[4]
+    vals[9], vals[10] = 1e-45, -1e-45  # g z rounds to zeros of both signs
+    ref = [b.clone() for b in base]
+    R.reconstruct(ref, seeds, vals, 1e-5, wd)
+    got = [b.clone() for b in base]
+    codec.directional_step([codec.ParamSpec(t, lr=1e-5, weight_decay=wd) for t in got], seeds, vals,
+                           stream_mode="torch_rocm")
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(zip(got, ref)):
+        an, bn = torch.isnan(a.float()), torch.isnan(b.float())
+        assert torch.equal(an, bn), f"tensor {i}: NaN positions differ"
+        _assert_same(torch.where(an, torch.zeros_like(a), a), torch.where(bn, torch.zeros_like(b), b), f"tensor {i}")
+
+
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
 def test_perturb_sequence_with_frozen_tensor(dtype):
     """random_perturb_parameters (optimizer.py:152-173) +1, -2, +1: frozen tensors draw
