@@ -1708,20 +1708,22 @@ int fks_host_jump_window(uint64_t seed, int64_t block, uint32_t* out624) {
 
 int fks_device_selfcheck(int32_t which, uint64_t* result, void* workspace, size_t ws_bytes, void* stream) {
   return guarded([&] {
-    if (!result || (which != FKS_CHECK_SQRT_DOMAIN && which != FKS_CHECK_PHILOX_RADIUS))
+    if (!result || (which != FKS_CHECK_SQRT_DOMAIN && which != FKS_CHECK_PHILOX_RADIUS &&
+                    which != FKS_CHECK_PHILOX_BF16_RADIUS))
       throw Error(-FKS_EINVAL, "bad arguments");
     const size_t need = sizeof(uint32_t) * (size_t)kSqrtDomainBlocks;
     if (!workspace || ws_bytes < need) throw Error(-FKS_EINVAL, "workspace too small");
     uint32_t* counts = static_cast<uint32_t*>(workspace);
-    int rc = which == FKS_CHECK_SQRT_DOMAIN ? launch_sqrt_domain_check(counts, stream)
-                                            : launch_philox_radius_check(counts, stream);
+    int rc = which == FKS_CHECK_SQRT_DOMAIN     ? launch_sqrt_domain_check(counts, stream)
+             : which == FKS_CHECK_PHILOX_RADIUS ? launch_philox_radius_check(counts, stream)
+                                                : launch_philox_fast_radius_check(counts, stream);
     if (rc) throw Error(-FKS_EHIP, std::string("self check launch: ") + hipGetErrorString((hipError_t)rc));
     std::vector<uint32_t> h((size_t)kSqrtDomainBlocks);
     if (hipMemcpyAsync(h.data(), counts, need, hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
         hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
       throw Error(-FKS_EHIP, "sqrt domain check copy");
     uint64_t bad = 0;
-    for (uint32_t v : h) bad += v;
+    for (uint32_t v : h) bad = which == FKS_CHECK_PHILOX_BF16_RADIUS ? std::max<uint64_t>(bad, v) : bad + v;
     *result = bad;
   });
 }

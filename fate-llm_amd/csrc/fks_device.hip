@@ -2512,6 +2512,17 @@ __device__ __forceinline__ float phx_cast(float v) {  // static_cast<scalar_t>(f
 // fks_device_selfcheck(FKS_CHECK_PHILOX_RADIUS) compares phx_radius2 with ocml's
 // sqrtf(-2 logf(u)) on all 2^32 words; tests/test_gpu_torch_rocm.py the whole stream with
 // torch.normal on the device.
+// The bf16 fast path's radius: x = RN(log2(u) RN(-2 ln 2)) in ONE rounding instead of
+// ocml's extended-precision r + e, then the raw v_sqrt_f32.  Within kPhxFastUlps ulps of
+// the exact radius on every one of the 2^32 words (fks_device_selfcheck
+// FKS_CHECK_PHILOX_BF16_RADIUS reports the largest distance; tests/test_gpu_selfcheck.py).
+constexpr uint32_t kPhxFastUlps = 2;
+__device__ __forceinline__ f32x2_t phx_radius2_fast(const f32x2_t u) {
+  const f32x2_t y = {__builtin_amdgcn_logf(u.x), __builtin_amdgcn_logf(u.y)};
+  const f32x2_t x = y * (f32x2_t){__uint_as_float(0xbfb17218u), __uint_as_float(0xbfb17218u)};  // RN(-2 ln 2)
+  return (f32x2_t){__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
+}
+
 template <bool kExact = true>
 __device__ __forceinline__ f32x2_t phx_radius2(const f32x2_t u) {
   const f32x2_t y = {__builtin_amdgcn_logf(u.x), __builtin_amdgcn_logf(u.y)};
@@ -2533,11 +2544,12 @@ __device__ __forceinline__ f32x2_t phx_radius2(const f32x2_t u) {
   return sq;
 }
 
-template <bool kExact = true>
+template <bool kExact = true, bool kFast = false>
 __device__ __forceinline__ void phx_box_muller2(const uint4 w, f32x2_t& zA, f32x2_t& zB) {
   const f32x2_t cu = {2.3283064e-10f, 2.3283064e-10f}, cv = {1.46291807e-09f, 1.46291807e-09f};
   const f32x2_t fx = {(float)w.x, (float)w.z}, fy = {(float)w.y, (float)w.w};
-  const f32x2_t sq = phx_radius2<kExact>(__builtin_elementwise_fma(fx, cu, cu));
+  const f32x2_t u = __builtin_elementwise_fma(fx, cu, cu);
+  const f32x2_t sq = kFast ? phx_radius2_fast(u) : phx_radius2<kExact>(u);
   const f32x2_t v = __builtin_elementwise_fma(fy, cv, cv);
   const f32x2_t rev = v * (f32x2_t){__uint_as_float(0x3e22f983u), __uint_as_float(0x3e22f983u)};  // 1/(2 pi)
   const f32x2_t sc1 = {__builtin_amdgcn_sinf(rev.x), __builtin_amdgcn_cosf(rev.x)};
@@ -2554,14 +2566,22 @@ __device__ __forceinline__ void phx_box_muller2(const uint4 w, f32x2_t& zA, f32x
 // rounding midpoint (low 16 bits 0x8000; across a binade both round to the power of two).
 // Lanes with any of their four products within 4 ulps of one redo the pair exactly (about
 // 3.5 % of the waves' iterations branch).
+// Window half-width W in f32 ulps around a bf16 rounding midpoint: a radius within k ulps
+// of the exact one moves z = RN(sc s) by at most 2k + 1 ulps (|sc| <= 1, the product's
+// ulp at most twice sc's ulp times s's), so W = 2k + 2: k = 1 for the raw root of the
+// exact x (W = 4), k = kPhxFastUlps for the one-rounding x (FKS_PHX_FAST_LOG).
+#ifndef FKS_PHX_FAST_LOG
+#define FKS_PHX_FAST_LOG 1
+#endif
+constexpr uint32_t kPhxMidW = FKS_PHX_FAST_LOG ? 2 * kPhxFastUlps + 2 : 4;
 __device__ __forceinline__ bool phx_near_bf16_mid(float z) {
-  return ((__float_as_uint(z) & 0xFFFFu) - 0x7FFCu) <= 8u;
+  return ((__float_as_uint(z) & 0xFFFFu) - (0x8000u - kPhxMidW)) <= 2 * kPhxMidW;
 }
 __device__ __forceinline__ void phx_z_bf16(const uint4 w, f32x2_t& zA, f32x2_t& zB) {
 #if FKS_PHX_EXACT_RADIUS  // A/B: the corrected radius always
   phx_box_muller2<true>(w, zA, zB);
 #else
-  phx_box_muller2<false>(w, zA, zB);
+  phx_box_muller2<false, FKS_PHX_FAST_LOG != 0>(w, zA, zB);
   const bool near = (int)phx_near_bf16_mid(zA.x) | (int)phx_near_bf16_mid(zA.y) | (int)phx_near_bf16_mid(zB.x) |
                     (int)phx_near_bf16_mid(zB.y);
   if (__builtin_expect(near, 0)) phx_box_muller2<true>(w, zA, zB);
@@ -2924,6 +2944,35 @@ __global__ __launch_bounds__(256) void fks_philox_radius_kernel(uint32_t* counts
   if (n) atomicAdd(&bad, n);
   __syncthreads();
   if (threadIdx.x == 0) counts[blockIdx.x] = bad;
+}
+
+// Device self check FKS_CHECK_PHILOX_BF16_RADIUS: the largest distance, in f32 ulps, of
+// the bf16 fast path's radius (phx_radius2_fast) from ocml's sqrtf(-2 logf(u)) over all
+// 2^32 words (both are >= +0, so the distance is the difference of the bit patterns);
+// one maximum per workgroup.
+__global__ __launch_bounds__(256) void fks_philox_fast_radius_kernel(uint32_t* counts) {
+  __shared__ uint32_t worst;
+  if (threadIdx.x == 0) worst = 0;
+  __syncthreads();
+  uint32_t m = 0;
+  const uint32_t base = (blockIdx.x * 256u + threadIdx.x) * 256u;
+  for (uint32_t i = 0; i < 256u; i += 2) {
+    const uint32_t x0 = base + i, x1 = base + i + 1;
+    const f32x2_t u = {__fmaf_rn((float)x0, 2.3283064e-10f, 2.3283064e-10f),
+                       __fmaf_rn((float)x1, 2.3283064e-10f, 2.3283064e-10f)};
+    const f32x2_t s = phx_radius2_fast(u);
+    const uint32_t a0 = __float_as_uint(s.x + 0.0f), b0 = __float_as_uint(phx_radius_ocml(x0) + 0.0f);
+    const uint32_t a1 = __float_as_uint(s.y + 0.0f), b1 = __float_as_uint(phx_radius_ocml(x1) + 0.0f);
+    m = max(m, max(a0 > b0 ? a0 - b0 : b0 - a0, a1 > b1 ? a1 - b1 : b1 - a1));
+  }
+  atomicMax(&worst, m);
+  __syncthreads();
+  if (threadIdx.x == 0) counts[blockIdx.x] = worst;
+}
+
+int launch_philox_fast_radius_check(uint32_t* counts, void* stream) {
+  hipLaunchKernelGGL(fks_philox_fast_radius_kernel, dim3(kSqrtDomainBlocks), dim3(256), 0, (hipStream_t)stream, counts);
+  return (int)hipGetLastError();
 }
 
 int launch_philox_radius_check(uint32_t* counts, void* stream) {

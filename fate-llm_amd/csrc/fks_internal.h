@@ -261,6 +261,7 @@ int launch_irregular(const IrrArgs& a, void* stream);
 constexpr int kSqrtDomainBlocks = (1 << 24) / 256;
 int launch_sqrt_domain_check(uint32_t* counts, void* stream);  // counts[kSqrtDomainBlocks]
 int launch_philox_radius_check(uint32_t* counts, void* stream);  // counts[kSqrtDomainBlocks]
+int launch_philox_fast_radius_check(uint32_t* counts, void* stream);  // per-block maxima
 int launch_delta_apply(const DeltaApplyDesc* d, int n, int64_t max_numel, const float* delta, void* stream);
 int device_cu_count();
 

@@ -18,6 +18,7 @@ HAS_WD, FROZEN, STREAM_ROCM = 1, 2, 4
 VALUE_SCALAR, VALUE_TENSOR = 0, 1
 CHECK_SQRT_DOMAIN = 1
 CHECK_PHILOX_RADIUS = 2
+CHECK_PHILOX_BF16_RADIUS = 3
 ABI_VERSION = 1
 
 # every symbol include/fks.h declares (checked by tests/test_capi_host.py)

@@ -264,6 +264,11 @@ int fks_host_tables(int32_t dtype, float* radius, float* cosv, float* sinv, int3
  * 2^32 words (up to the sign of a zero, which the following "+ 0" erases); same
  * workspace. */
 #define FKS_CHECK_PHILOX_RADIUS 2
+/* FKS_CHECK_PHILOX_BF16_RADIUS: *result = the largest distance in f32 ulps, over all 2^32
+ * words, of the radius the torch_rocm kernel's bf16 fast path computes (log2(u) times
+ * RN(-2 ln 2) in one rounding, raw v_sqrt_f32) from ocml's sqrtf(-2 logf(u)); the kernel's
+ * bf16 midpoint window assumes at most 2.  Same workspace. */
+#define FKS_CHECK_PHILOX_BF16_RADIUS 3
 int fks_device_selfcheck(int32_t which, uint64_t* result, void* workspace, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus

@@ -42,6 +42,24 @@ def test_philox_radius_equals_ocml_on_all_words():
     assert bad.value == 0
 
 
+def test_philox_bf16_fast_radius_within_two_ulps():
+    """The bf16 fast path's radius (one-rounding -2 ln(u), raw v_sqrt_f32) stays within 2
+    f32 ulps of ocml's sqrtf(-2 logf(u)) on all 2^32 words -- the bound phx_z_bf16's
+    midpoint window (W = 2 k + 2 = 6 ulps) is built on."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from fate_llm.algo.fedkseed import _native as N
+    L = N.load()
+    dev = torch.device("cuda", 0)
+    ws = torch.empty(1 << 18, dtype=torch.uint8, device=dev)
+    worst = ctypes.c_uint64(123)
+    with torch.cuda.device(dev):
+        N.check(L.fks_device_selfcheck(N.CHECK_PHILOX_BF16_RADIUS, ctypes.byref(worst), ws.data_ptr(), ws.numel(),
+                                       torch.cuda.current_stream(dev).cuda_stream))
+    print(f"largest radius distance: {worst.value} ulps")
+    assert worst.value <= 2
+
+
 def test_selfcheck_rejects_bad_arguments():
     from fate_llm.algo.fedkseed import _native as N
     L = N.load()
