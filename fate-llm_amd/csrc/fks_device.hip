@@ -1179,6 +1179,40 @@ __device__ __forceinline__ f32x2_t apply_pair(f32x2_t p, f32x2_t z, float g, flo
   return z;
 }
 
+// f16 parameters in the torch_rocm stream.  The reference then runs torch's DEVICE
+// kernels, and hipcc compiles their Half "f32 scalar * f16 tensor" (an f32 product cast to
+// Half) into v_fma_mixlo_f16 a, b, 0: ONE rounding of the exact product (+0) -- where
+// c10::Half on the CPU (the torch_cpu stream, apply_pair) rounds the f32 product first,
+// and the two differ when that f32 product lands on an f16 rounding midpoint (and in the
+// sign of a zero product).  Every scalar product of the chain -- g z, wd p, lr t, and the
+// perturbation's ps z (zo_utils.py:49-52, optimizer.py:173) -- is therefore the same
+// instruction here; the sums of two f16 values round the same either way.
+__device__ __forceinline__ float mul_f16_dev(float a, float b) {  // a, b as f32 (b f16-exact)
+  uint32_t r = 0;
+  asm volatile("v_fma_mixlo_f16 %0, %1, %2, 0" : "+v"(r) : "v"(a), "v"(b));
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)(r & 0xffffu));
+}
+template <int MODE>
+__device__ __forceinline__ f32x2_t apply_pair_f16dev(f32x2_t p, f32x2_t z, float g, float lr, float wd, bool has_wd,
+                                                     float ps, bool upd) {
+  float q[2] = {p.x, p.y};
+  const float zz[2] = {z.x, z.y};
+  const bool use_wd = MODE == kModeUpdateNoWd ? false
+                      : (MODE == kModeUpdateWd || MODE == kModeUpdateWd0 || MODE == kModeUpdateWdPos0) ? true
+                                                                                                          : has_wd;
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    if (MODE == kModePerturb || MODE == kModePerturbUpdate) {
+      q[i] = rhf(q[i] + mul_f16_dev(ps, zz[i]));
+      if (MODE == kModePerturb || !upd) continue;
+    }
+    const float gz = mul_f16_dev(g, zz[i]);
+    const float t = use_wd ? rhf(gz + mul_f16_dev(wd, q[i])) : gz;
+    q[i] = rhf(q[i] - mul_f16_dev(lr, t));
+  }
+  return (f32x2_t){q[0], q[1]};
+}
+
 template <int DT>
 __device__ __forceinline__ f32x2_t z_pair2(const uint8_t* lds, uint32_t r1, uint32_t r2) {
   f32x2_t z;
@@ -2644,6 +2678,9 @@ __device__ __forceinline__ void phx_item(const PhiloxArgs& a, const PhxTensor& T
     if (MODE == kModeWriteZ) {
       pA = zA;
       pB = zB;
+    } else if constexpr (DT == FKS_F16) {  // the device kernels' single-rounding products
+      pA = apply_pair_f16dev<MODE>(pA, zA, g, T.lr, T.wd, has_wd, T.ps, upd);
+      pB = apply_pair_f16dev<MODE>(pB, zB, g, T.lr, T.wd, has_wd, T.ps, upd);
     } else {
       pA = apply_pair<DT, MODE>(pA, zA, g, T.lr, T.wd, has_wd, T.ps, upd);
       pB = apply_pair<DT, MODE>(pB, zB, g, T.lr, T.wd, has_wd, T.ps, upd);

@@ -7,6 +7,11 @@ not the reference): after torch.manual_seed(seed), torch.normal(..., device="cud
 each tensor in order, and the reference's update expression as torch ops on the device
 (oracle/torch_replica.py).  Bar: bit-exact.
 
+f16 on the device: hipcc compiles torch's Half "f32 scalar * f16 tensor" into
+v_fma_mixlo_f16 (one rounding of the exact product), unlike c10::Half on the CPU (two);
+the kernel follows the device (fks_device.hip mul_f16_dev), which
+test_zero_weight_decay_edge_values caught: g z = 37.390625 in f32, an f16 midpoint.
+
 Cases: fp32 / bf16 / f16; tensors below one 256-thread block, between blocks, past the
 grid cap (several Philox calls per thread), empty tensors in the list (no draw, no
 offset); several seeds including 0, 2^32-1 and one past 2^32; reconstructs at weight
@@ -56,7 +61,7 @@ def _params(dtype, dev, seed=0):
     return [(torch.randn(s, generator=g) * 0.02).to(DT[dtype]).to(dev) for s in shapes]
 
 
-@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16", "float16"])
 @pytest.mark.parametrize("wd", [0.01, 0.0, None])
 def test_reconstruct_matches_torch_on_device(dtype, wd):
     """ClientTrainer.train_once's loop (fedkseed.py:136-141) run by the reference's own
@@ -120,7 +125,7 @@ def test_zero_weight_decay_edge_values(wd, gscale, keep_fma, monkeypatch):
         _assert_same(torch.where(an, torch.zeros_like(a), a), torch.where(bn, torch.zeros_like(b), b), f"tensor {i}")
 
 
-@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16", "float16"])
 def test_perturb_sequence_with_frozen_tensor(dtype):
     """random_perturb_parameters (optimizer.py:152-173) +1, -2, +1: frozen tensors draw
     nothing; the restore is not bit-exact (three roundings), the same in both."""
