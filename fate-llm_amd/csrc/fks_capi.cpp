@@ -982,7 +982,7 @@ void phx_geometry(const fks_tensor* t, int nt, const double* scales, PhxPlan* P)
       x.dtype = t[i].dtype;
       x.lr = t[i].lr;
       x.wd = t[i].wd;
-      x.flags = t[i].flags & FKS_HAS_WD;
+      x.flags = (t[i].flags & FKS_HAS_WD) | (((uintptr_t)t[i].data % 16u) == 0 ? kPhxP16 : 0u);
       x.ps = scales ? (float)scales[i] : 0.0f;
       tab.push_back(x);
       elem0.push_back(elems - n);
@@ -1124,6 +1124,7 @@ void run_philox(const fks_tensor* t, int nt, const uint64_t* seeds, const double
         a.g[3 * j + d] = value_kind == FKS_VALUE_TENSOR ? round_to_dtype(values[s0 + j], d) : (float)values[s0 + j];
     }
     a.nseeds = nb;
+    a.call_first = s0 == 0 ? 1 : 0;
     const int rc = timed(0, stream, [&] { return launch_philox(a, stream); });
     if (rc) throw Error(rc < 0 ? rc : -FKS_EHIP, std::string("fks_philox_kernel launch: ") +
                                                      (rc > 0 ? hipGetErrorString((hipError_t)rc) : "unsupported"));

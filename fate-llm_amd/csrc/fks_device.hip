@@ -1180,21 +1180,31 @@ __device__ __forceinline__ f32x2_t apply_pair(f32x2_t p, f32x2_t z, float g, flo
 }
 
 // f16 parameters in the torch_rocm stream.  The reference then runs torch's DEVICE
-// kernels, and hipcc compiles their Half "f32 scalar * f16 tensor" (an f32 product cast to
-// Half) into v_fma_mixlo_f16 a, b, 0: ONE rounding of the exact product (+0) -- where
-// c10::Half on the CPU (the torch_cpu stream, apply_pair) rounds the f32 product first,
-// and the two differ when that f32 product lands on an f16 rounding midpoint (and in the
-// sign of a zero product).  Every scalar product of the chain -- g z, wd p, lr t, and the
-// perturbation's ps z (zo_utils.py:49-52, optimizer.py:173) -- is therefore the same
-// instruction here; the sums of two f16 values round the same either way.
-__device__ __forceinline__ float mul_f16_dev(float a, float b) {  // a, b as f32 (b f16-exact)
-  uint32_t r = 0;
-  asm volatile("v_fma_mixlo_f16 %0, %1, %2, 0" : "+v"(r) : "v"(a), "v"(b));
-  return (float)__builtin_bit_cast(_Float16, (uint16_t)(r & 0xffffu));
+// elementwise kernels (ATen/native/cuda/CUDALoops.cuh), and how those round a Half
+// "f32 scalar * f16 tensor" product depends on the code path (measured on this image,
+// tools/diag_f16_tail.py, profiles/r05_f16_rounding.log):
+//   * the 8-wide vectorized path -- every pointer 16-byte aligned, elements below
+//     N - N % 2048 (full blocks of 256 threads x 8) -- rounds the f32 product to f16:
+//     TWICE, like c10::Half on the CPU;
+//   * the unrolled path -- the partial last block, or a tensor that is not 16-byte aligned
+//     -- is compiled to v_fma_mixlo_f16 a, b, 0: ONE rounding of the exact product.
+// The two differ when the f32 product lands on an f16 rounding midpoint (and in the sign of
+// a zero product).  The chain's products: g z, lr t and the perturbation's ps z read fresh,
+// aligned tensors (z, t); wd p reads the parameter -- its own alignment at the call's first
+// seed, a fresh aligned tensor after it (the reference rebinds param.data every step,
+// zo_utils.py:49).  The sums of two f16 values round the same either way.
+__device__ __forceinline__ float mul_f16_ref(float a, float b, bool once) {  // b f16-exact
+  if (once) {
+    uint32_t r = 0;
+    asm volatile("v_fma_mixlo_f16 %0, %1, %2, 0" : "+v"(r) : "v"(a), "v"(b));
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)(r & 0xffffu));
+  }
+  return rhf(a * b);
 }
 template <int MODE>
 __device__ __forceinline__ f32x2_t apply_pair_f16dev(f32x2_t p, f32x2_t z, float g, float lr, float wd, bool has_wd,
-                                                     float ps, bool upd) {
+                                                     float ps, bool upd, const bool (&once)[2],
+                                                     const bool (&wd_once)[2]) {
   float q[2] = {p.x, p.y};
   const float zz[2] = {z.x, z.y};
   const bool use_wd = MODE == kModeUpdateNoWd ? false
@@ -1203,12 +1213,12 @@ __device__ __forceinline__ f32x2_t apply_pair_f16dev(f32x2_t p, f32x2_t z, float
 #pragma unroll
   for (int i = 0; i < 2; i++) {
     if (MODE == kModePerturb || MODE == kModePerturbUpdate) {
-      q[i] = rhf(q[i] + mul_f16_dev(ps, zz[i]));
+      q[i] = rhf(q[i] + mul_f16_ref(ps, zz[i], once[i]));
       if (MODE == kModePerturb || !upd) continue;
     }
-    const float gz = mul_f16_dev(g, zz[i]);
-    const float t = use_wd ? rhf(gz + mul_f16_dev(wd, q[i])) : gz;
-    q[i] = rhf(q[i] - mul_f16_dev(lr, t));
+    const float gz = mul_f16_ref(g, zz[i], once[i]);
+    const float t = use_wd ? rhf(gz + mul_f16_ref(wd, q[i], wd_once[i])) : gz;
+    q[i] = rhf(q[i] - mul_f16_ref(lr, t, once[i]));
   }
   return (f32x2_t){q[0], q[1]};
 }
@@ -2658,6 +2668,13 @@ __device__ __forceinline__ void phx_item(const PhiloxArgs& a, const PhxTensor& T
   const float gd = dv ? dev_value_g<DT>(a.gdev) : 0.0f;
   const PhxRound1 r1 = philox_round1(T.off4 + j, idx);
   f32x2_t pA = {p[0], p[1]}, pB = {p[2], p[3]};
+  // f16: which elements torch's unrolled path (one rounding) takes (mul_f16_ref)
+  bool tail[4] = {false, false, false, false};
+  const bool p16 = (T.flags & kPhxP16) != 0;
+  if (DT == FKS_F16) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) tail[i] = e[i] >= T.numel - T.numel % kTorchHalfBlockWork;
+  }
   for (int k = 0; k < a.nseeds; k++) {
     const uint64_t seed = a.seeds[k];  // wave-uniform: scalar loads
     const float g = dv ? gd : a.g[3 * k + DT];
@@ -2678,9 +2695,16 @@ __device__ __forceinline__ void phx_item(const PhiloxArgs& a, const PhxTensor& T
     if (MODE == kModeWriteZ) {
       pA = zA;
       pB = zB;
-    } else if constexpr (DT == FKS_F16) {  // the device kernels' single-rounding products
-      pA = apply_pair_f16dev<MODE>(pA, zA, g, T.lr, T.wd, has_wd, T.ps, upd);
-      pB = apply_pair_f16dev<MODE>(pB, zB, g, T.lr, T.wd, has_wd, T.ps, upd);
+    } else if constexpr (DT == FKS_F16) {  // torch's device rounding of the products (mul_f16_ref)
+      // wd p at the call's first seed reads the caller's parameter (its alignment); later
+      // seeds read the reference's freshly allocated, aligned result.  (kModePerturbUpdate's
+      // update follows the restore perturbation, whose result is fresh.)
+      const bool first = a.call_first && k == 0 && MODE != kModePerturbUpdate;
+      const bool wA[2] = {tail[0] || (first && !p16), tail[1] || (first && !p16)};
+      const bool wB[2] = {tail[2] || (first && !p16), tail[3] || (first && !p16)};
+      const bool oA[2] = {tail[0], tail[1]}, oB[2] = {tail[2], tail[3]};
+      pA = apply_pair_f16dev<MODE>(pA, zA, g, T.lr, T.wd, has_wd, T.ps, upd, oA, wA);
+      pB = apply_pair_f16dev<MODE>(pB, zB, g, T.lr, T.wd, has_wd, T.ps, upd, oB, wB);
     } else {
       pA = apply_pair<DT, MODE>(pA, zA, g, T.lr, T.wd, has_wd, T.ps, upd);
       pB = apply_pair<DT, MODE>(pB, zB, g, T.lr, T.wd, has_wd, T.ps, upd);

@@ -222,10 +222,16 @@ struct PhxTensor {
   int32_t dtype;
   float lr;
   float wd;
-  uint32_t flags;   // FKS_HAS_WD | FKS_FROZEN
+  uint32_t flags;   // FKS_HAS_WD | kPhxP16
   float ps;         // perturbation scale (perturb modes)
 };
 static_assert(sizeof(PhxTensor) == 56, "PhxTensor layout");
+// PhxTensor::flags: the parameter's data is 16-byte aligned (an f16 tensor then takes torch's
+// 8-wide vectorized elementwise path; fks_device.hip mul_f16_ref)
+constexpr uint32_t kPhxP16 = 1u << 8;
+// torch's elementwise kernels on ROCm (ATen/native/cuda/CUDALoops.cuh): a 2-byte tensor is
+// processed in blocks of 256 threads x 8 elements; a partial last block takes the unrolled path
+constexpr int64_t kTorchHalfBlockWork = 2048;
 
 constexpr int kPhxSeeds = 32;  // seeds per launch (by value in the arguments)
 struct PhiloxArgs {
@@ -238,7 +244,7 @@ struct PhiloxArgs {
   int32_t nt;
   int32_t nseeds;
   int32_t mode;
-  int32_t pad;
+  int32_t call_first;   // seed 0 of this launch is the first seed of the call
 };
 int launch_philox(const PhiloxArgs& a, void* stream);
 int device_max_threads_per_cu();

@@ -7,10 +7,13 @@ not the reference): after torch.manual_seed(seed), torch.normal(..., device="cud
 each tensor in order, and the reference's update expression as torch ops on the device
 (oracle/torch_replica.py).  Bar: bit-exact.
 
-f16 on the device: hipcc compiles torch's Half "f32 scalar * f16 tensor" into
-v_fma_mixlo_f16 (one rounding of the exact product), unlike c10::Half on the CPU (two);
-the kernel follows the device (fks_device.hip mul_f16_dev), which
-test_zero_weight_decay_edge_values caught: g z = 37.390625 in f32, an f16 midpoint.
+f16 on the device: torch's elementwise kernels round a Half "f32 scalar * f16 tensor"
+product twice (f32, then f16) on their 8-wide vectorized path and once (v_fma_mixlo_f16)
+on the unrolled path -- the partial last block of 2048 elements, or a tensor not 16-byte
+aligned (profiles/r05_f16_rounding.log); the kernel follows both (fks_device.hip
+mul_f16_ref).  test_zero_weight_decay_edge_values caught it: g z = 37.390625 in f32, an
+f16 midpoint, in the tail of a 5647-element tensor; test_f16_products_follow_torchs_paths
+crafts such midpoints everywhere.
 
 Cases: fp32 / bf16 / f16; tensors below one 256-thread block, between blocks, past the
 grid cap (several Philox calls per thread), empty tensors in the list (no draw, no
@@ -123,6 +126,31 @@ def test_zero_weight_decay_edge_values(wd, gscale, keep_fma, monkeypatch):
         an, bn = torch.isnan(a.float()), torch.isnan(b.float())
         assert torch.equal(an, bn), f"tensor {i}: NaN positions differ"
         _assert_same(torch.where(an, torch.zeros_like(a), a), torch.where(bn, torch.zeros_like(b), b), f"tensor {i}")
+
+
+@pytest.mark.parametrize("n", [5647, 177489, 1000003])
+@pytest.mark.parametrize("off", [0, 1])
+@pytest.mark.parametrize("wd", [None, 0.01])
+def test_f16_products_follow_torchs_paths(n, off, wd):
+    """f16 parameters, many products: about one in 10^4 f32 products g z / lr t / wd p lands
+    on an f16 rounding midpoint, where torch's vectorized path (full 2048-element blocks
+    of 16-byte-aligned tensors) and its unrolled path (the partial last block, unaligned
+    tensors) round differently.  The parameter is a view at element offset `off` of a
+    larger buffer (off 1: 2-byte aligned: the first seed's wd p takes the unrolled path in
+    the reference).  Against the reference's expression as torch ops on the device."""
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    gen = torch.Generator(dev).manual_seed(n + off)
+    buf = (torch.randn(n + off + 64, device=dev, generator=gen) * 0.05).to(torch.float16)
+    ref_buf, got_buf = buf.clone(), buf.clone()
+    ref, got = [ref_buf[off:off + n]], got_buf[off:off + n]
+    g = torch.Generator().manual_seed(9)
+    seeds = torch.randint(0, 2**32, (8,), generator=g).tolist()
+    vals = (torch.randn(8, generator=g, dtype=torch.float64) * 20).tolist()
+    R.reconstruct(ref, seeds, vals, 1e-3, wd)
+    codec.directional_step([codec.ParamSpec(got, lr=1e-3, weight_decay=wd)], seeds, vals, stream_mode="torch_rocm")
+    torch.cuda.synchronize()
+    _assert_same(got, ref[0], f"n {n} off {off} wd {wd}")
 
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16", "float16"])
