@@ -2223,6 +2223,9 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   // for task n - FKS_BS_LAG before twisting task n.  Half 1's task m needs half 0's task
   // m + 2 kBsWaves (publish_stored), so the bound must exceed 2 kBsWaves = 12.
   static_assert(FKS_BS_LAG == 0 || FKS_BS_LAG > 2 * kBsWaves, "FKS_BS_LAG: half 1 trails by 12 tasks");
+  // only the weight-decay chains need it: the wd 0 / None chains keep half 1 within L2 reach
+  // unaided (4.17 B/param), and there the bound measured 1.4 % slower (profiles/r05d_ab_lag.log)
+  constexpr bool kLag = FKS_BS_LAG > 0 && (MODE == kModeUpdateWd || MODE == kModeUpdate);
   const uint32_t prog1 = kBsProg1Off + 4u * (uint32_t)hw;
   auto publish_applied = [&](const int m) {
     if (lane == 0) *(volatile lds_u32_t*)(size_t)prog1 = (uint32_t)m + 1u;
@@ -2237,7 +2240,7 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
   // into nx (past the last task: the sink)
   auto task = [&](const int n, const Slot& sl, Slot& nx) {
     uint32_t oa[8], ob[8];
-    if (FKS_BS_LAG > 0 && ordered && half == 0) await_applied(n - FKS_BS_LAG);
+    if (kLag && ordered && half == 0) await_applied(n - FKS_BS_LAG);
     __builtin_amdgcn_s_setprio(2);
 #if !FKS_BS_DIAG_NOWAIT  // diagnostic (wrong values): no hand-off wait, the resource bound
     while (__builtin_amdgcn_readfirstlane(bs_flag_load(flag)) < (uint32_t)n) __builtin_amdgcn_s_sleep(0);
@@ -2257,7 +2260,7 @@ __global__ __launch_bounds__(kBsThreads, 1) void fks_apply_bs_kernel(ApplyBsArgs
 #else
     chain(sl, oa, ob);
 #endif
-    if (FKS_BS_LAG > 0 && ordered && half) publish_applied(n);
+    if (kLag && ordered && half) publish_applied(n);
   };
 
   // two named slots and a loop unrolled by two: a slot copy on the back edge would wait

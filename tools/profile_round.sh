@@ -9,7 +9,7 @@
 # 2) the default bench line (N=1, with cpu_baseline)      -> gpurun_out/${TAG}_bench_default.log
 # 3) rocprofv3 --kernel-trace --stats of one bench step   -> gpurun_out/${TAG}_trace/
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
 PMCV=${PMCV:-wd0 full}
 TAG=$TAG VARIANTS="$PMCV" timeout -k 10 600 bash tools/gpu_pmc2.sh > gpurun_out/${TAG}_pmc.log 2>&1 || { tail gpurun_out/${TAG}_pmc.log; exit 91; }
 for v in $PMCV; do cp profiles/pmc_apply_${TAG}_$v.json gpurun_out/ 2>/dev/null; done
