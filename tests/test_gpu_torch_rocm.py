@@ -243,3 +243,87 @@ def test_element_shards_are_contiguous_runs_census(nshards):
             counts[i] += int(wr[i])
     assert ends[-1] == total
     assert counts == [0 if fz else n for n, fz in zip(sizes, frozen)]
+
+
+def _reference_zo_steps(groups, seeds, losses, eps):
+    """The reference's ZerothOrderOptimizer.zeroth_order_step (optimizer.py:113-148, its
+    random_perturb_parameters :152-173) and zo_utils.directional_derivative_step
+    (zo_utils.py:42-52) as torch ops on the parameters' device: frozen tensors draw no
+    perturbation but are updated; the first group's lr and wd hold for every group."""
+    rets, it = [], iter(losses)
+
+    def perturb(seed, sf):
+        torch.manual_seed(seed)
+        for grp in groups:
+            for p in grp["params"]:
+                if p.requires_grad:
+                    z = torch.normal(mean=0, std=1, size=p.data.size(), device=p.data.device, dtype=p.data.dtype)
+                    p.data = p.data + sf * eps * z
+
+    for seed in seeds:
+        perturb(seed, 1.0)
+        right = next(it)
+        perturb(seed, -2.0)
+        left = next(it)
+        perturb(seed, 1.0)
+        if torch.isnan(right) or torch.isnan(left):
+            rets.append(float("nan"))
+            continue
+        g = (right - left) / (2 * eps)
+        torch.manual_seed(seed)
+        lr = wd = None
+        for grp in groups:
+            wd = grp["weight_decay"] if wd is None else wd
+            lr = grp["lr"] if lr is None else lr
+            for p in grp["params"]:
+                z = torch.normal(mean=0, std=1, size=p.data.size(), device=p.data.device, dtype=p.data.dtype)
+                p.data = p.data - lr * (g * z + wd * p.data)
+        rets.append(float(g))
+    return rets
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16", "float16"])
+@pytest.mark.parametrize("wd0", [0.0, 0.01])
+@pytest.mark.parametrize("path", ["device", "host", "frozen"])
+def test_zo_steps_match_the_reference_on_device(dtype, wd0, path):
+    """The drop-in optimizer's local steps on a GPU client, under the default stream
+    setting ("auto" -> torch_rocm for cuda tensors), against the reference's steps as torch
+    ops on the same GPU: four steps with device losses, the third with a NaN loss (restore,
+    no update); the fused device tail (losses stay on the device), the host tail, and a
+    group holding a frozen tensor (perturb skips it, the update does not; unfused)."""
+    from fate_llm.algo.fedkseed import codec
+    from fate_llm.algo.fedkseed.optimizer import ZerothOrderOptimizer
+    dev = _dev()
+    eps = 5e-4
+    data = _params(dtype, dev, seed=21)
+    frozen = [False] * len(data)
+    if path == "frozen":
+        frozen[2] = True
+    seeds = [7, 2**32 - 1, 123456789, 2**40 + 5]
+    loss_vals = [2.5, 2.25, 2.375, 2.5, float("nan"), 2.0, 3.0, 2.875]
+
+    def build():
+        ps = [torch.nn.Parameter(t.clone(), requires_grad=not fz) for t, fz in zip(data, frozen)]
+        return ps, [{"params": ps[:3], "weight_decay": wd0, "lr": 1e-3, "eps": eps},
+                    {"params": ps[3:], "weight_decay": 0.01 - wd0, "lr": 2e-3, "eps": eps}]
+
+    ref, ref_groups = build()
+    want = _reference_zo_steps(ref_groups, seeds, [torch.tensor(x, device=dev) for x in loss_vals], eps)
+    got, groups = build()
+    old = codec.get_stream_mode()
+    codec.set_stream_mode("auto")
+    try:
+        opt = ZerothOrderOptimizer(groups, lr=1e-3, eps=eps, weight_decay=wd0, grad_clip=-100.0)
+        opt.device_step = path == "device"
+        it = iter([torch.tensor(x, device=dev) for x in loss_vals])
+        rets = []
+        for s in seeds:
+            g, _, _ = opt.zeroth_order_step(s, lambda: next(it))
+            assert opt._last_step_on_device == (path == "device")
+            rets.append(float(g))
+    finally:
+        codec.set_stream_mode(old)
+    torch.cuda.synchronize()
+    assert [str(x) for x in rets] == [str(x) for x in want]
+    for i, (a, b) in enumerate(zip(got, ref)):
+        _assert_same(a.data, b.data, f"tensor {i}")
