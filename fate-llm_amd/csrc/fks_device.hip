@@ -2646,25 +2646,15 @@ __device__ __forceinline__ float phx_radius_ocml(uint32_t x) {
 // The item's four elements through every seed of the pass, in seed order, as two packed
 // pairs (apply_pair: the values of apply_one); MODE may be a launch-wide weight-decay
 // specialisation of kModeUpdate (kModeUpdateWd / NoWd / Wd0, as the CPU stream's kernels).
+// (phx_seeds: the seed loop of work item (idx, j) on its four elements e[i], values p[i])
 template <int DT, int MODE_>
-__device__ __forceinline__ void phx_item(const PhiloxArgs& a, const PhxTensor& T, int64_t r) {
+__device__ __forceinline__ void phx_seeds(const PhiloxArgs& a, const PhxTensor& T, uint32_t idx, uint64_t j,
+                                          const int64_t e[4], float p[4]) {
   // (the host gives kModeUpdateWdPos0 launches bf16 / f32 tensors only)
   constexpr int MODE = (MODE_ == kModeUpdateWdPos0 && DT == FKS_F16) ? (int)kModeUpdateWd0 : MODE_;
-  using TR = Traits<DT>;
-  const uint32_t S = T.stride;
-  const uint32_t idx = (uint32_t)(r % S);
-  const uint64_t j = (uint64_t)(r / S);
-  int64_t e[4];
-  bool on[4];
-  float p[4];
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    e[i] = (int64_t)idx + (int64_t)S * (int64_t)(4 * j + i);
-    on[i] = e[i] < T.numel;
-    p[i] = (MODE != kModeWriteZ && on[i]) ? TR::load(T.ptr, e[i]) : 0.0f;
-    // kModeUpdateWdPos0: a +-inf parameter is NaN after the reference's first seed (wd * p)
+  for (int i = 0; i < 4; i++)  // kModeUpdateWdPos0: a +-inf parameter is NaN after the reference's first seed (wd p)
     if (MODE == kModeUpdateWdPos0 && __builtin_isinf(p[i])) p[i] = __builtin_nanf("");
-  }
   const bool has_wd = (T.flags & FKS_HAS_WD) != 0;
   const bool dv = MODE == kModePerturbUpdate && a.gdev;
   const bool upd = dv ? dev_value_apply(a.gdev) : true;
@@ -2714,9 +2704,108 @@ __device__ __forceinline__ void phx_item(const PhiloxArgs& a, const PhxTensor& T
     }
   }
   p[0] = pA.x; p[1] = pA.y; p[2] = pB.x; p[3] = pB.y;
+}
+
+template <int DT, int MODE>
+__device__ __forceinline__ void phx_item(const PhiloxArgs& a, const PhxTensor& T, int64_t r) {
+  using TR = Traits<DT>;
+  const uint32_t S = T.stride;
+  const uint32_t idx = (uint32_t)(r % S);
+  const uint64_t j = (uint64_t)(r / S);
+  int64_t e[4];
+  bool on[4];
+  float p[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    e[i] = (int64_t)idx + (int64_t)S * (int64_t)(4 * j + i);
+    on[i] = e[i] < T.numel;
+    p[i] = (MODE != kModeWriteZ && on[i]) ? TR::load(T.ptr, e[i]) : 0.0f;
+  }
+  phx_seeds<DT, MODE>(a, T, idx, j, e, p);
 #pragma unroll
   for (int i = 0; i < 4; i++)
     if (on[i]) TR::store(T.ptr, e[i], p[i]);
+}
+
+// kPhxVec consecutive work items (idx0 .. idx0 + 7 of one row j; item boundaries of
+// tensors and shards are multiples of 256): element i of each lies in the 8-element run
+// idx0 + S (4 j + i) + [0, 8), so the eight items load and store as four 16-byte runs
+// (bf16 / f16; two each for f32) instead of 32 single-element accesses.  A call of few
+// seeds is bound by the memory accesses in flight, not by the VALU: this is its form
+// (the item loop above issues 2-byte loads, 128 bytes per wave instruction).
+constexpr int kPhxVec = 8;
+typedef __attribute__((address_space(1))) u32x4_t gu128;
+
+template <int DT>
+__device__ __forceinline__ void phx_load8(uint64_t ptr, int64_t e, float v[kPhxVec]) {
+  const gu128* q = reinterpret_cast<const gu128*>(ptr + (uint64_t)e * (DT == FKS_F32 ? 4 : 2));
+  if constexpr (DT == FKS_F32) {
+    const u32x4_t x = q[0], y = q[1];
+    const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = __uint_as_float(w[i]);
+  } else {
+    const u32x4_t x = q[0];
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      v[2 * i] = Traits<DT>::cvt(w[i] & 0xffffu);
+      v[2 * i + 1] = Traits<DT>::cvt(w[i] >> 16);
+    }
+  }
+}
+
+template <int DT>
+__device__ __forceinline__ void phx_store8(uint64_t ptr, int64_t e, const float v[kPhxVec]) {
+  gu128* q = reinterpret_cast<gu128*>(ptr + (uint64_t)e * (DT == FKS_F32 ? 4 : 2));
+  if constexpr (DT == FKS_F32) {
+    q[0] = (u32x4_t){__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+    q[1] = (u32x4_t){__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])};
+  } else {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) w[i] = Traits<DT>::pack(Traits<DT>::bits(v[2 * i]), Traits<DT>::bits(v[2 * i + 1]));
+    q[0] = (u32x4_t){w[0], w[1], w[2], w[3]};
+  }
+}
+
+template <int DT, int MODE>
+__device__ __forceinline__ void phx_vitem(const PhiloxArgs& a, const PhxTensor& T, int64_t r0) {
+  const uint32_t S = T.stride;
+  const uint32_t idx0 = (uint32_t)(r0 % S);
+  const uint64_t j = (uint64_t)(r0 / S);
+  const int64_t e0 = (int64_t)idx0 + (int64_t)S * (int64_t)(4 * j);
+  // whole runs only: 16-byte aligned data (idx0 and S are multiples of 8) and every element
+  // of the four runs inside the tensor; else (a tensor's last row, unaligned data) per item
+  if (!(T.flags & kPhxP16) || e0 + 3 * (int64_t)S + kPhxVec > T.numel) {
+    for (int q = 0; q < kPhxVec; q++) phx_item<DT, MODE>(a, T, r0 + q);
+    return;
+  }
+  float v[4][kPhxVec];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    if (MODE == kModeWriteZ) {
+#pragma unroll
+      for (int q = 0; q < kPhxVec; q++) v[i][q] = 0.0f;
+    } else {
+      phx_load8<DT>(T.ptr, e0 + (int64_t)S * i, v[i]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kPhxVec; q++) {
+    int64_t e[4];
+    float p[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      e[i] = e0 + (int64_t)S * i + q;
+      p[i] = v[i][q];
+    }
+    phx_seeds<DT, MODE>(a, T, idx0 + (uint32_t)q, j, e, p);
+#pragma unroll
+    for (int i = 0; i < 4; i++) v[i][q] = p[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) phx_store8<DT>(T.ptr, e0 + (int64_t)S * i, v[i]);
 }
 
 template <int MODE>
@@ -2735,6 +2824,29 @@ __global__ __launch_bounds__(256) void fks_philox_kernel(PhiloxArgs a) {
       case FKS_F32: phx_item<FKS_F32, MODE>(a, T, it - T.item0); break;
       case FKS_BF16: phx_item<FKS_BF16, MODE>(a, T, it - T.item0); break;
       default: phx_item<FKS_F16, MODE>(a, T, it - T.item0); break;
+    }
+  }
+}
+
+// fks_philox_kernel over kPhxVec-item groups (phx_vitem): the launch form of calls of few
+// seeds (the ZO step's perturb / restore + update, K-small reconstructs)
+template <int MODE>
+__global__ __launch_bounds__(256) void fks_philox_vec_kernel(PhiloxArgs a) {
+  const int64_t step = (int64_t)gridDim.x * blockDim.x * kPhxVec;
+  int t0 = 0;
+  for (int64_t it = a.item_lo + ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kPhxVec; it < a.item_hi;
+       it += step) {
+    int lo = t0, hi = a.nt - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (a.t[mid].item0 <= it) lo = mid; else hi = mid - 1;
+    }
+    t0 = lo;
+    const PhxTensor T = a.t[lo];
+    switch (T.dtype) {
+      case FKS_F32: phx_vitem<FKS_F32, MODE>(a, T, it - T.item0); break;
+      case FKS_BF16: phx_vitem<FKS_BF16, MODE>(a, T, it - T.item0); break;
+      default: phx_vitem<FKS_F16, MODE>(a, T, it - T.item0); break;
     }
   }
 }
@@ -3056,11 +3168,27 @@ int device_max_threads_per_cu() {
   return n;
 }
 
+// calls of at most this many seeds per launch take fks_philox_vec_kernel
+// (FKS_PHX_VEC_MAXK overrides; 0 turns it off)
+static int phx_vec_maxk() {
+  static const int v = [] {
+    const char* s = std::getenv("FKS_PHX_VEC_MAXK");
+    return (s && *s) ? std::atoi(s) : 4;
+  }();
+  return v;
+}
+
 template <int MODE>
 static int launch_philox_m(const PhiloxArgs& a, void* stream) {
   const int64_t items = a.item_hi - a.item_lo;
+  if (items <= 0) return 0;
+  if (a.nseeds <= phx_vec_maxk() && a.item_lo % kPhxVec == 0 && items % kPhxVec == 0) {
+    const int64_t vitems = items / kPhxVec;
+    const int64_t blocks = std::min<int64_t>((vitems + 255) / 256, (int64_t)device_cu_count() * 16);
+    hipLaunchKernelGGL((fks_philox_vec_kernel<MODE>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+    return (int)hipGetLastError();
+  }
   const int64_t blocks = std::min<int64_t>((items + 255) / 256, (int64_t)device_cu_count() * 16);
-  if (blocks <= 0) return 0;
   hipLaunchKernelGGL((fks_philox_kernel<MODE>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }

@@ -66,14 +66,17 @@ def _params(dtype, dev, seed=0):
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16", "float16"])
 @pytest.mark.parametrize("wd", [0.01, 0.0, None])
-def test_reconstruct_matches_torch_on_device(dtype, wd):
+@pytest.mark.parametrize("k", [40, 37])
+def test_reconstruct_matches_torch_on_device(dtype, wd, k):
     """ClientTrainer.train_once's loop (fedkseed.py:136-141) run by the reference's own
-    arithmetic on the GPU vs the codec's reconstruct in the torch_rocm stream."""
+    arithmetic on the GPU vs the codec's reconstruct in the torch_rocm stream.  k 40: two
+    item-loop launches (32 + 7 non-zero seeds); k 37: 32 + 4, the second launch in the
+    few-seed form (fks_philox_vec_kernel, FKS_PHX_VEC_MAXK = 4)."""
     from fate_llm.algo.fedkseed import codec
     dev = _dev()
     g = torch.Generator().manual_seed(7)
-    seeds = torch.randint(0, 2**32, (40,), generator=g).tolist()
-    vals = (torch.randn(40, generator=g, dtype=torch.float64) * 20).tolist()
+    seeds = torch.randint(0, 2**32, (k,), generator=g).tolist()
+    vals = (torch.randn(k, generator=g, dtype=torch.float64) * 20).tolist()
     vals[5] = 0.0
     ref = _params(dtype, dev)
     got = [p.clone() for p in ref]
@@ -131,7 +134,8 @@ def test_zero_weight_decay_edge_values(wd, gscale, keep_fma, monkeypatch):
 @pytest.mark.parametrize("n", [5647, 177489, 1000003])
 @pytest.mark.parametrize("off", [0, 1])
 @pytest.mark.parametrize("wd", [None, 0.01])
-def test_f16_products_follow_torchs_paths(n, off, wd):
+@pytest.mark.parametrize("k", [8, 3])
+def test_f16_products_follow_torchs_paths(n, off, wd, k):
     """f16 parameters, many products: about one in 10^4 f32 products g z / lr t / wd p lands
     on an f16 rounding midpoint, where torch's vectorized path (full 2048-element blocks
     of 16-byte-aligned tensors) and its unrolled path (the partial last block, unaligned
@@ -145,8 +149,8 @@ def test_f16_products_follow_torchs_paths(n, off, wd):
     ref_buf, got_buf = buf.clone(), buf.clone()
     ref, got = [ref_buf[off:off + n]], got_buf[off:off + n]
     g = torch.Generator().manual_seed(9)
-    seeds = torch.randint(0, 2**32, (8,), generator=g).tolist()
-    vals = (torch.randn(8, generator=g, dtype=torch.float64) * 20).tolist()
+    seeds = torch.randint(0, 2**32, (k,), generator=g).tolist()  # k 3: fks_philox_vec_kernel
+    vals = (torch.randn(k, generator=g, dtype=torch.float64) * 20).tolist()
     R.reconstruct(ref, seeds, vals, 1e-3, wd)
     codec.directional_step([codec.ParamSpec(got, lr=1e-3, weight_decay=wd)], seeds, vals, stream_mode="torch_rocm")
     torch.cuda.synchronize()
