@@ -71,7 +71,7 @@ VALU_MIX_CEILING_TLANEOPS = 1024 * 64 * 2.4e9 / VALU_MIX_CYCLES / 1e12
 # per-launch counters of the bf16 slice kernel (fks_apply_bs_kernel), tools/summarize_pmc2.py: the
 # weight-decay chain (wd != 0) and the zero-weight-decay chain (kModeUpdateWd0)
 PMC_SUMMARIES = {"wd": "pmc_apply_r05_full.json", "wd0": "pmc_apply_r05_wd0.json"}
-# the torch_rocm stream's kernel (fks_philox_kernel, 32-seed launches) at wd 0.0
+# the torch_rocm stream's kernel (fks_philox_vec_kernel, 32-seed launches) at wd 0.0
 PMC_SUMMARY_PHX = "pmc_apply_r05_phx_wd0.json"
 
 
@@ -133,7 +133,7 @@ def load_pmc_summary(wd=None, name=None):
 def alt_stream_leg(codec, views, ks, kv, wd, total, build_id):
     """The same 7B reconstruct drawn from the torch_rocm stream -- the z a reference client
     draws when its model sits on an MI355X (zo_utils.py:47: device=param.data.device) --
-    timed once, with the VALU roofline of its kernel (fks_philox_kernel)."""
+    timed once, with the VALU roofline of its kernel (fks_philox_vec_kernel)."""
     specs = [codec.ParamSpec(v, lr=1e-5, weight_decay=wd) for v in views]
     codec.directional_step(specs, ks[:32], kv[:32], stream_mode="torch_rocm")  # the tensor table
     torch.cuda.synchronize()
@@ -142,7 +142,7 @@ def alt_stream_leg(codec, views, ks, kv, wd, total, build_id):
         codec.directional_step(specs, ks, kv, stream_mode="torch_rocm")
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    out = {"stream": "torch_rocm", "kernel": "fks_philox_kernel", "weight_decay": wd, "steps": 1,
+    out = {"stream": "torch_rocm", "kernel": "fks_philox_vec_kernel", "weight_decay": wd, "steps": 1,
            "ms_per_step": round(dt * 1e3, 1), "value": round(total * 2 / dt / 1e9, 4), "unit": "GB/s",
            "ms_per_seed": round(dt * 1e3 / len(ks), 3), "launches": prof.n_apply,
            "kernel_ms": round(prof.apply_ms, 1)}

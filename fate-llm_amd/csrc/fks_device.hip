@@ -2731,8 +2731,9 @@ __device__ __forceinline__ void phx_item(const PhiloxArgs& a, const PhxTensor& T
 // tensors and shards are multiples of 256): element i of each lies in the 8-element run
 // idx0 + S (4 j + i) + [0, 8), so the eight items load and store as four 16-byte runs
 // (bf16 / f16; two each for f32) instead of 32 single-element accesses.  A call of few
-// seeds is bound by the memory accesses in flight, not by the VALU: this is its form
-// (the item loop above issues 2-byte loads, 128 bytes per wave instruction).
+// seeds is bound by the memory accesses in flight, not by the VALU (the item loop above
+// issues 2-byte loads, 128 bytes per wave instruction: a one-seed perturb of the 7B layout
+// took 20.9 ms there, 7.2 ms here; profiles/r05h_smallk_rocm_maxk*.log).
 constexpr int kPhxVec = 8;
 typedef __attribute__((address_space(1))) u32x4_t gu128;
 
@@ -3168,12 +3169,13 @@ int device_max_threads_per_cu() {
   return n;
 }
 
-// calls of at most this many seeds per launch take fks_philox_vec_kernel
-// (FKS_PHX_VEC_MAXK overrides; 0 turns it off)
+// launches of at most this many seeds take fks_philox_vec_kernel: every launch by default
+// (7B bf16 wd 0, 32-seed launches: 4.39 against 4.57 ms per seed in the item loop;
+// profiles/r05i_rocm_rate_vec_ab.log); FKS_PHX_VEC_MAXK=0 restores the item loop (A/B)
 static int phx_vec_maxk() {
   static const int v = [] {
     const char* s = std::getenv("FKS_PHX_VEC_MAXK");
-    return (s && *s) ? std::atoi(s) : 4;
+    return (s && *s) ? std::atoi(s) : kPhxSeeds;
   }();
   return v;
 }

@@ -69,9 +69,8 @@ def _params(dtype, dev, seed=0):
 @pytest.mark.parametrize("k", [40, 37])
 def test_reconstruct_matches_torch_on_device(dtype, wd, k):
     """ClientTrainer.train_once's loop (fedkseed.py:136-141) run by the reference's own
-    arithmetic on the GPU vs the codec's reconstruct in the torch_rocm stream.  k 40: two
-    item-loop launches (32 + 7 non-zero seeds); k 37: 32 + 4, the second launch in the
-    few-seed form (fks_philox_vec_kernel, FKS_PHX_VEC_MAXK = 4)."""
+    arithmetic on the GPU vs the codec's reconstruct in the torch_rocm stream.  k 40:
+    launches of 32 + 7 non-zero seeds; k 37: 32 + 4."""
     from fate_llm.algo.fedkseed import codec
     dev = _dev()
     g = torch.Generator().manual_seed(7)
@@ -149,7 +148,7 @@ def test_f16_products_follow_torchs_paths(n, off, wd, k):
     ref_buf, got_buf = buf.clone(), buf.clone()
     ref, got = [ref_buf[off:off + n]], got_buf[off:off + n]
     g = torch.Generator().manual_seed(9)
-    seeds = torch.randint(0, 2**32, (k,), generator=g).tolist()  # k 3: fks_philox_vec_kernel
+    seeds = torch.randint(0, 2**32, (k,), generator=g).tolist()
     vals = (torch.randn(k, generator=g, dtype=torch.float64) * 20).tolist()
     R.reconstruct(ref, seeds, vals, 1e-3, wd)
     codec.directional_step([codec.ParamSpec(got, lr=1e-3, weight_decay=wd)], seeds, vals, stream_mode="torch_rocm")

@@ -4,7 +4,7 @@
 # One rocprofv3 pass per counter group; results under gpurun_out/pmc2_<variant>_<group>/.
 # PERF_ARGS (tools/perf_one.py arguments), PERF_STREAM, PMC_SEEDS (seeds per launch) and
 # PMC_KERNEL (kernel-name substring for the summary) select another kernel, e.g. the
-# torch_rocm stream: PERF_STREAM=torch_rocm PMC_SEEDS=32 PMC_KERNEL=fks_philox_kernel.
+# torch_rocm stream: PERF_STREAM=torch_rocm PMC_SEEDS=32 PMC_KERNEL=fks_philox_vec_kernel.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 GROUPS_=("SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU2 SQ_INSTS_VALU GRBM_GUI_ACTIVE"
          "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_CVT SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 GRBM_GUI_ACTIVE"

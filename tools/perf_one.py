@@ -1,7 +1,7 @@
 """One reconstruct of K seeds over an N-param buffer, twice, for kernel timing /
 counter collection (rocprofv3 around it).  python tools/perf_one.py [bf16|f32] [log2 N] [K]
 Defaults: bf16, N = 2^30, weight decay PERF_WD (default 0.01) (chunks as long as the 7B bench's order of magnitude), K = 19;
-PERF_STREAM=torch_rocm draws the torch_rocm stream (fks_philox_kernel)."""
+PERF_STREAM=torch_rocm draws the torch_rocm stream (fks_philox_vec_kernel)."""
 import os
 import sys
 

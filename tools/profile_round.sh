@@ -14,7 +14,7 @@ PMCV=${PMCV:-wd0 full}
 TAG=$TAG VARIANTS="$PMCV" timeout -k 10 600 bash tools/gpu_pmc2.sh > gpurun_out/${TAG}_pmc.log 2>&1 || { tail gpurun_out/${TAG}_pmc.log; exit 91; }
 for v in $PMCV; do cp profiles/pmc_apply_${TAG}_$v.json gpurun_out/ 2>/dev/null; done
 if [ -z "$NO_PHX" ]; then
-  PERF_STREAM=torch_rocm PERF_ARGS="bf16 28 64" PMC_SEEDS=32 PMC_KERNEL=fks_philox_kernel TAG=${TAG}_phx VARIANTS=wd0 \
+  PERF_STREAM=torch_rocm PERF_ARGS="bf16 28 64" PMC_SEEDS=32 PMC_KERNEL=fks_philox_vec_kernel TAG=${TAG}_phx VARIANTS=wd0 \
     timeout -k 10 600 bash tools/gpu_pmc2.sh > gpurun_out/${TAG}_pmc_phx.log 2>&1 || { tail gpurun_out/${TAG}_pmc_phx.log; exit 94; }
   cp profiles/pmc_apply_${TAG}_phx_wd0.json gpurun_out/
 fi
