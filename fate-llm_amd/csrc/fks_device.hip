@@ -2734,13 +2734,28 @@ __device__ __forceinline__ void phx_item(const PhiloxArgs& a, const PhxTensor& T
 // seeds is bound by the memory accesses in flight, not by the VALU (the item loop above
 // issues 2-byte loads, 128 bytes per wave instruction: a one-seed perturb of the 7B layout
 // took 20.9 ms there, 7.2 ms here; profiles/r05h_smallk_rocm_maxk*.log).
-constexpr int kPhxVec = 8;
+#ifndef FKS_PHX_VEC_ITEMS
+#define FKS_PHX_VEC_ITEMS 8
+#endif
+constexpr int kPhxVec = FKS_PHX_VEC_ITEMS;  // 8 (A/B: 4)
+static_assert(kPhxVec == 4 || kPhxVec == 8, "16- or 8-byte runs of 2-byte elements");
 typedef __attribute__((address_space(1))) u32x4_t gu128;
+
+typedef __attribute__((address_space(1))) u32x2_t gu64v;
 
 template <int DT>
 __device__ __forceinline__ void phx_load8(uint64_t ptr, int64_t e, float v[kPhxVec]) {
   const gu128* q = reinterpret_cast<const gu128*>(ptr + (uint64_t)e * (DT == FKS_F32 ? 4 : 2));
-  if constexpr (DT == FKS_F32) {
+  if constexpr (kPhxVec == 4) {
+    if constexpr (DT == FKS_F32) {
+      const u32x4_t x = q[0];
+      v[0] = __uint_as_float(x.x); v[1] = __uint_as_float(x.y); v[2] = __uint_as_float(x.z); v[3] = __uint_as_float(x.w);
+    } else {
+      const u32x2_t x = *reinterpret_cast<const gu64v*>(q);
+      v[0] = Traits<DT>::cvt(x.x & 0xffffu); v[1] = Traits<DT>::cvt(x.x >> 16);
+      v[2] = Traits<DT>::cvt(x.y & 0xffffu); v[3] = Traits<DT>::cvt(x.y >> 16);
+    }
+  } else if constexpr (DT == FKS_F32) {
     const u32x4_t x = q[0], y = q[1];
     const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
 #pragma unroll
@@ -2759,7 +2774,14 @@ __device__ __forceinline__ void phx_load8(uint64_t ptr, int64_t e, float v[kPhxV
 template <int DT>
 __device__ __forceinline__ void phx_store8(uint64_t ptr, int64_t e, const float v[kPhxVec]) {
   gu128* q = reinterpret_cast<gu128*>(ptr + (uint64_t)e * (DT == FKS_F32 ? 4 : 2));
-  if constexpr (DT == FKS_F32) {
+  if constexpr (kPhxVec == 4) {
+    if constexpr (DT == FKS_F32) {
+      q[0] = (u32x4_t){__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+    } else {
+      *reinterpret_cast<gu64v*>(q) = (u32x2_t){Traits<DT>::pack(Traits<DT>::bits(v[0]), Traits<DT>::bits(v[1])),
+                                               Traits<DT>::pack(Traits<DT>::bits(v[2]), Traits<DT>::bits(v[3]))};
+    }
+  } else if constexpr (DT == FKS_F32) {
     q[0] = (u32x4_t){__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
     q[1] = (u32x4_t){__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])};
   } else {
@@ -2809,6 +2831,56 @@ __device__ __forceinline__ void phx_vitem(const PhiloxArgs& a, const PhxTensor& 
   for (int i = 0; i < 4; i++) phx_store8<DT>(T.ptr, e0 + (int64_t)S * i, v[i]);
 }
 
+// FKS_PHX_VEC_PREFETCH (A/B): the next group's 16-byte runs (2-byte dtypes) are loaded
+// before this group's seed loop, so that a wave keeps its loads in flight while it computes
+#ifndef FKS_PHX_VEC_PREFETCH
+#define FKS_PHX_VEC_PREFETCH 0
+#endif
+template <int MODE>
+__device__ __forceinline__ bool phx_prefetch(const PhxTensor& T, int64_t r0, u32x4_t raw[4]) {
+  if (MODE == kModeWriteZ || T.dtype == FKS_F32 || kPhxVec != 8) return false;
+  const uint32_t S = T.stride;
+  const int64_t e0 = (int64_t)(uint32_t)(r0 % S) + (int64_t)S * (int64_t)(4 * (uint64_t)(r0 / S));
+  if (!(T.flags & kPhxP16) || e0 + 3 * (int64_t)S + kPhxVec > T.numel) return false;
+#pragma unroll
+  for (int i = 0; i < 4; i++) raw[i] = *reinterpret_cast<const gu128*>(T.ptr + (uint64_t)(e0 + (int64_t)S * i) * 2);
+  return true;
+}
+
+template <int DT, int MODE>
+__device__ __forceinline__ void phx_vitem_pre(const PhiloxArgs& a, const PhxTensor& T, int64_t r0,
+                                              const u32x4_t raw[4]) {
+  const uint32_t S = T.stride;
+  const uint32_t idx0 = (uint32_t)(r0 % S);
+  const uint64_t j = (uint64_t)(r0 / S);
+  const int64_t e0 = (int64_t)idx0 + (int64_t)S * (int64_t)(4 * j);
+  float v[4][kPhxVec];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t w[4] = {raw[i].x, raw[i].y, raw[i].z, raw[i].w};
+#pragma unroll
+    for (int c = 0; c < 4 && 2 * c + 1 < kPhxVec; c++) {
+      v[i][2 * c] = Traits<DT>::cvt(w[c] & 0xffffu);
+      v[i][2 * c + 1] = Traits<DT>::cvt(w[c] >> 16);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kPhxVec; q++) {
+    int64_t e[4];
+    float p[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      e[i] = e0 + (int64_t)S * i + q;
+      p[i] = v[i][q];
+    }
+    phx_seeds<DT, MODE>(a, T, idx0 + (uint32_t)q, j, e, p);
+#pragma unroll
+    for (int i = 0; i < 4; i++) v[i][q] = p[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) phx_store8<DT>(T.ptr, e0 + (int64_t)S * i, v[i]);
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void fks_philox_kernel(PhiloxArgs a) {
   const int64_t step = (int64_t)gridDim.x * blockDim.x;
@@ -2831,9 +2903,57 @@ __global__ __launch_bounds__(256) void fks_philox_kernel(PhiloxArgs a) {
 
 // fks_philox_kernel over kPhxVec-item groups (phx_vitem): the launch form of calls of few
 // seeds (the ZO step's perturb / restore + update, K-small reconstructs)
+#if defined(FKS_PHX_VEC_WPE) && FKS_PHX_VEC_WPE > 0  // A/B: a waves-per-SIMD floor (caps the VGPRs)
+#define FKS_PHX_VEC_ATTR __attribute__((amdgpu_waves_per_eu(FKS_PHX_VEC_WPE)))
+#else
+#define FKS_PHX_VEC_ATTR
+#endif
+__device__ __forceinline__ int phx_find(const PhiloxArgs& a, int64_t it, int lo) {
+  int hi = a.nt - 1;  // the last tensor whose first item is <= it (items only grow)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (a.t[mid].item0 <= it) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
 template <int MODE>
-__global__ __launch_bounds__(256) void fks_philox_vec_kernel(PhiloxArgs a) {
+__global__ __launch_bounds__(256) FKS_PHX_VEC_ATTR void fks_philox_vec_kernel(PhiloxArgs a) {
   const int64_t step = (int64_t)gridDim.x * blockDim.x * kPhxVec;
+#if FKS_PHX_VEC_PREFETCH
+  int64_t it = a.item_lo + ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kPhxVec;
+  if (it >= a.item_hi) return;
+  int ti = phx_find(a, it, 0);
+  u32x4_t raw[4];
+  bool pre = phx_prefetch<MODE>(a.t[ti], it - a.t[ti].item0, raw);
+  while (true) {
+    const PhxTensor T = a.t[ti];
+    const int64_t nit = it + step;
+    int nti = ti;
+    u32x4_t nraw[4];
+    bool npre = false;
+    if (nit < a.item_hi) {
+      nti = phx_find(a, nit, ti);
+      npre = phx_prefetch<MODE>(a.t[nti], nit - a.t[nti].item0, nraw);
+    }
+    if (pre) {
+      if (T.dtype == FKS_BF16) phx_vitem_pre<FKS_BF16, MODE>(a, T, it - T.item0, raw);
+      else phx_vitem_pre<FKS_F16, MODE>(a, T, it - T.item0, raw);
+    } else {
+      switch (T.dtype) {
+        case FKS_F32: phx_vitem<FKS_F32, MODE>(a, T, it - T.item0); break;
+        case FKS_BF16: phx_vitem<FKS_BF16, MODE>(a, T, it - T.item0); break;
+        default: phx_vitem<FKS_F16, MODE>(a, T, it - T.item0); break;
+      }
+    }
+    if (nit >= a.item_hi) break;
+    it = nit;
+    ti = nti;
+    pre = npre;
+#pragma unroll
+    for (int i = 0; i < 4; i++) raw[i] = nraw[i];
+  }
+#else
   int t0 = 0;
   for (int64_t it = a.item_lo + ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kPhxVec; it < a.item_hi;
        it += step) {
@@ -2850,6 +2970,7 @@ __global__ __launch_bounds__(256) void fks_philox_vec_kernel(PhiloxArgs a) {
       default: phx_vitem<FKS_F16, MODE>(a, T, it - T.item0); break;
     }
   }
+#endif
 }
 
 // ------------------------------------------------------------------ delta apply
