@@ -259,7 +259,7 @@ int fks_host_tables(int32_t dtype, float* radius, float* cosv, float* sinv, int3
  * workspace >= 262,144 bytes. */
 #define FKS_CHECK_SQRT_DOMAIN 1
 /* FKS_CHECK_PHILOX_RADIUS: the torch_rocm stream's Box-Muller radius sqrt(-2 log u) as
- * fks_philox_kernel computes it (trimmed to the inputs Philox can give) must equal
+ * the torch_rocm kernels compute it (trimmed to the inputs Philox can give) must equal
  * ocml's general sqrtf(-2 logf(u)), the instructions torch's device kernel runs, on all
  * 2^32 words (up to the sign of a zero, which the following "+ 0" erases); same
  * workspace. */
