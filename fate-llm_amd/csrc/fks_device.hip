@@ -2917,10 +2917,118 @@ __device__ __forceinline__ int phx_find(const PhiloxArgs& a, int64_t it, int lo)
   return lo;
 }
 
+// FKS_PHX_VEC_UNIFORM: the tensor of a wave's 64 groups is looked up once per wave, with
+// wave-uniform indices, instead of a per-lane binary search whose dependent vector loads
+// each wait for every load and store in flight (vmcnt is in order); 2 (default): from a
+// copy of the tensor table in LDS (launches of at most kPhxLdsTensors tensors).  One-seed
+// perturb of the 7B layout: 7.07 (0, per-lane search) / 6.86-7.30 (1) / 6.41-6.45 ms (2),
+// 32-seed launches unchanged (profiles/r05k_phx_vec_uniform_ab.log)
+#ifndef FKS_PHX_VEC_UNIFORM
+#define FKS_PHX_VEC_UNIFORM 2
+#endif
+constexpr int kPhxLdsTensors = 512;
+__device__ __forceinline__ int64_t rfl64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+template <class Tab>
+__device__ __forceinline__ int phx_find_t(Tab tab, int nt, int64_t it, int lo, int probes) {
+  // the last tensor whose first item is <= it, at or after lo (items only grow; a wave's
+  // next groups lie mostly in the same or the next tensor: a few probes, then bisection)
+  for (int p = 0; p < probes; p++) {
+    if (lo + 1 >= nt || tab[lo + 1].item0 > it) return lo;
+    ++lo;
+  }
+  int hi = nt - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[mid].item0 <= it) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+template <int MODE, class Tab>
+__device__ __forceinline__ void phx_vec_uniform(const PhiloxArgs& a, Tab tab, int64_t step) {
+  const int lane = (int)(threadIdx.x & 63u);
+  int64_t wb = rfl64(a.item_lo + ((int64_t)blockIdx.x * blockDim.x + (int64_t)(threadIdx.x & ~63u)) * kPhxVec);
+  int ts = 0;
+  // this lane's group of the wave's groups from wb, and its tensor (ts: the wave's first)
+  auto lane_tensor = [&](int64_t w, int t, int64_t& it) {
+    const int64_t wend = w + 64 * kPhxVec < a.item_hi ? w + 64 * kPhxVec : a.item_hi;
+    const bool one = t + 1 >= a.nt || tab[t + 1].item0 >= wend;  // the whole wave in tensor t
+    it = w + (int64_t)lane * kPhxVec;
+    return one ? t : phx_find_t(tab, a.nt, it < a.item_hi ? it : a.item_hi - 1, t, 0);
+  };
+#if FKS_PHX_VEC_PREFETCH
+  u32x4_t raw[4];
+  bool pre = false;
+  if (wb < a.item_hi) {
+    ts = __builtin_amdgcn_readfirstlane(phx_find_t(tab, a.nt, wb, ts, 2));
+    int64_t it;
+    const int ti = lane_tensor(wb, ts, it);
+    if (it < a.item_hi) pre = phx_prefetch<MODE>(tab[ti], it - tab[ti].item0, raw);
+  }
+#endif
+  for (; wb < a.item_hi; wb += step) {
+    ts = __builtin_amdgcn_readfirstlane(phx_find_t(tab, a.nt, wb, ts, 2));
+    int64_t it;
+    const int ti = lane_tensor(wb, ts, it);
+#if FKS_PHX_VEC_PREFETCH
+    const PhxTensor T = tab[ti];  // (read before the prefetch: a global table read waits on vmcnt)
+    // the next groups' runs, loaded before this group's seed loop
+    u32x4_t nraw[4];
+    bool npre = false;
+    const int64_t nwb = wb + step;
+    if (nwb < a.item_hi) {
+      const int nts = __builtin_amdgcn_readfirstlane(phx_find_t(tab, a.nt, nwb, ts, 2));
+      int64_t nit;
+      const int nti = lane_tensor(nwb, nts, nit);
+      if (nit < a.item_hi) npre = phx_prefetch<MODE>(tab[nti], nit - tab[nti].item0, nraw);
+    }
+    if (it < a.item_hi) {
+      if (pre) {
+        if (T.dtype == FKS_BF16) phx_vitem_pre<FKS_BF16, MODE>(a, T, it - T.item0, raw);
+        else phx_vitem_pre<FKS_F16, MODE>(a, T, it - T.item0, raw);
+      } else {
+        switch (T.dtype) {
+          case FKS_F32: phx_vitem<FKS_F32, MODE>(a, T, it - T.item0); break;
+          case FKS_BF16: phx_vitem<FKS_BF16, MODE>(a, T, it - T.item0); break;
+          default: phx_vitem<FKS_F16, MODE>(a, T, it - T.item0); break;
+        }
+      }
+    }
+    pre = npre;
+#pragma unroll
+    for (int i = 0; i < 4; i++) raw[i] = nraw[i];
+#else
+    if (it >= a.item_hi) continue;
+    const PhxTensor T = tab[ti];
+    switch (T.dtype) {
+      case FKS_F32: phx_vitem<FKS_F32, MODE>(a, T, it - T.item0); break;
+      case FKS_BF16: phx_vitem<FKS_BF16, MODE>(a, T, it - T.item0); break;
+      default: phx_vitem<FKS_F16, MODE>(a, T, it - T.item0); break;
+    }
+#endif
+  }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) FKS_PHX_VEC_ATTR void fks_philox_vec_kernel(PhiloxArgs a) {
   const int64_t step = (int64_t)gridDim.x * blockDim.x * kPhxVec;
-#if FKS_PHX_VEC_PREFETCH
+#if FKS_PHX_VEC_UNIFORM
+#if FKS_PHX_VEC_UNIFORM == 2
+  extern __shared__ PhxTensor s_tab[];
+  if (a.nt <= kPhxLdsTensors) {
+    constexpr int W = (int)(sizeof(PhxTensor) / 4);
+    for (int i = (int)threadIdx.x; i < a.nt * W; i += (int)blockDim.x)
+      reinterpret_cast<uint32_t*>(s_tab)[i] = reinterpret_cast<const uint32_t*>(a.t)[i];
+    __syncthreads();
+    phx_vec_uniform<MODE>(a, s_tab, step);
+    return;
+  }
+#endif
+  phx_vec_uniform<MODE>(a, a.t, step);
+#elif FKS_PHX_VEC_PREFETCH
   int64_t it = a.item_lo + ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kPhxVec;
   if (it >= a.item_hi) return;
   int ti = phx_find(a, it, 0);
@@ -3308,7 +3416,8 @@ static int launch_philox_m(const PhiloxArgs& a, void* stream) {
   if (a.nseeds <= phx_vec_maxk() && a.item_lo % kPhxVec == 0 && items % kPhxVec == 0) {
     const int64_t vitems = items / kPhxVec;
     const int64_t blocks = std::min<int64_t>((vitems + 255) / 256, (int64_t)device_cu_count() * 16);
-    hipLaunchKernelGGL((fks_philox_vec_kernel<MODE>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+    const size_t lds = (FKS_PHX_VEC_UNIFORM == 2 && a.nt <= kPhxLdsTensors) ? sizeof(PhxTensor) * (size_t)a.nt : 0;
+    hipLaunchKernelGGL((fks_philox_vec_kernel<MODE>), dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, a);
     return (int)hipGetLastError();
   }
   const int64_t blocks = std::min<int64_t>((items + 255) / 256, (int64_t)device_cu_count() * 16);

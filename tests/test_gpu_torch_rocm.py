@@ -330,3 +330,29 @@ def test_zo_steps_match_the_reference_on_device(dtype, wd0, path):
     assert [str(x) for x in rets] == [str(x) for x in want]
     for i, (a, b) in enumerate(zip(got, ref)):
         _assert_same(a.data, b.data, f"tensor {i}")
+
+
+@pytest.mark.parametrize("nt", [300, 600])
+def test_tensor_tables_in_and_out_of_lds(nt):
+    """fks_philox_vec_kernel looks tensors up in an LDS copy of the table for launches of at
+    most 512 tensors and in device memory beyond: both against the reference as torch ops,
+    with sizes that put tensor boundaries inside a wave's 64 groups (per-lane lookups)."""
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    g = torch.Generator().manual_seed(nt)
+    sizes = torch.randint(1, 6000, (nt,), generator=g).tolist()
+    sizes[nt // 2] = 300_000
+    ref = [(torch.randn(n, generator=g) * 0.02).to(torch.bfloat16).to(dev) for n in sizes]
+    got = [p.clone() for p in ref]
+    seeds = torch.randint(0, 2**32, (35,), generator=g).tolist()
+    vals = (torch.randn(35, generator=g, dtype=torch.float64) * 20).tolist()
+    R.reconstruct(ref, seeds, vals, 1e-3, 0.01)
+    codec.directional_step([codec.ParamSpec(p, lr=1e-3, weight_decay=0.01) for p in got], seeds, vals,
+                           stream_mode="torch_rocm")
+    codec.perturb(got, seeds[0], 5e-4, stream_mode="torch_rocm")
+    torch.manual_seed(seeds[0])
+    for i, p in enumerate(ref):
+        ref[i] = p + 5e-4 * torch.normal(mean=0, std=1, size=p.size(), device=p.device, dtype=p.dtype)
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(zip(got, ref)):
+        _assert_same(a, b, f"tensor {i}")
