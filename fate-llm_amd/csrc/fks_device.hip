@@ -930,7 +930,26 @@ __device__ __forceinline__ void cephes_sincosf_nonneg(float x, float& s, float& 
 // measured 3 % slower: profiles/r04h_sqrt_ab.log.  v_sqrt_f64 rounded to f32 -- three
 // instructions, no select -- is 4.7 % faster but NOT correctly rounded: the self check
 // counts 1,326,243 of the 2^24 inputs wrong, profiles/r04i_sqrt64.log.)
+#ifndef FKS_SQRT_F64NR
+#define FKS_SQRT_F64NR 0
+#endif
+#if FKS_SQRT_F64NR
+// (A/B) the root in double: v_rsq_f64 (relative error <= 2^-22), two Newton steps with the
+// fixed half-reciprocal (error ~1.5 e^3 < 2^-60, then one f64 rounding), one rounding to
+// float -- the correctly rounded root, as sqrt of a 24-bit float lies at least ~2^-49
+// (relative) from an f32 rounding midpoint; +-0 passes through (sqrt(+-0) = +-0)
+__device__ __forceinline__ float radius_sqrt(float x) {
+  const double d = (double)x;
+  const double t = __builtin_amdgcn_rsq(d);
+  const double h = 0.5 * t;
+  double s = d * t;
+  s = __builtin_fma(__builtin_fma(-s, s, d), h, s);
+  s = __builtin_fma(__builtin_fma(-s, s, d), h, s);
+  return x == 0.0f ? x : (float)s;
+}
+#else
 __device__ __forceinline__ float radius_sqrt(float x) { return sqrtf(x); }
+#endif
 
 __device__ __forceinline__ void z_pair_f32_raw(uint32_t r1, uint32_t r2, float& z1, float& z2) {
   u32x2_t w;
