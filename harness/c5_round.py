@@ -162,12 +162,13 @@ class _Steps(torch.utils.data.Dataset):
         return {"input_ids": torch.zeros(1, dtype=torch.long)}
 
 
-PREFIX = 4096  # parameters of the first tensor a --record client reports
+PREFIX = 4096  # parameters of the first tensor a --record client reports (--record-prefix)
 
 
-def _prefix_bits(model):
-    """The first PREFIX elements of the model's first parameter, as raw bits (bf16: u16)."""
-    t = next(model.parameters()).detach().reshape(-1)[:PREFIX]
+def _prefix_bits(model, n=PREFIX):
+    """The first n elements (0: all) of the model's first parameter, as raw bits (bf16: u16)."""
+    t = next(model.parameters()).detach().reshape(-1)
+    t = t[:n] if n else t
     return t.view(torch.int16).cpu().numpy().view("u2").tolist()
 
 
@@ -187,7 +188,7 @@ def run_client(rank, args, arbiter_rank):
     raw = _Ctx([], arbiter_rank)
     ctx = WireContext(raw) if args.wire else raw
     timings, received_all, histories = [], [], []
-    records = {"model_0": _prefix_bits(model_0), "rounds": []} if args.record else None
+    records = {"model_0": _prefix_bits(model_0, args.record_prefix), "rounds": []} if args.record else None
     steps = []  # this round's local steps: (seed, g as returned -- a device or host value --, group-0 lr)
     if args.record:
         orig_step = OPT.ZerothOrderOptimizer.zeroth_order_step
@@ -235,7 +236,7 @@ def run_client(rank, args, arbiter_rank):
                        "seeds_reconstructed": n}
             if records is not None:
                 self._model = model
-                self._after_reconstruct = _prefix_bits(model)
+                self._after_reconstruct = _prefix_bits(model, args.record_prefix)
             return model
 
         def train_once(self, seed_candidates, seed_probabilities, direction_derivative_sum):
@@ -276,7 +277,7 @@ def run_client(rank, args, arbiter_rank):
                     "probabilities": torch.as_tensor(seed_probabilities).float().tolist(),
                     "after_reconstruct": self._after_reconstruct,
                     "steps": [(sd, float(torch.as_tensor(g).reshape(()).item()), lr) for sd, g, lr in steps],
-                    "after_steps": _prefix_bits(self._model),
+                    "after_steps": _prefix_bits(self._model, args.record_prefix),
                     "history": hist})
                 self._model = None
             return hist
@@ -368,6 +369,8 @@ def main(argv=None):
     ap.add_argument("--driver", choices=("optimizer", "trainer"), default="optimizer")
     ap.add_argument("--wire", action="store_true", help="round payloads in the compact binary format")
     ap.add_argument("--record", action="store_true", help="return every client's round for an oracle replay")
+    ap.add_argument("--record-prefix", type=int, default=PREFIX,
+                    help="parameters of the first tensor --record reports (0: the whole tensor)")
     args = ap.parse_args(argv)
     if args.resident:
         args.placement = "device"

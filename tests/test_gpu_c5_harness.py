@@ -115,6 +115,67 @@ def test_eight_clients_trainer_loop_wire():
     assert checked == 8 * rounds * steps
 
 
+def test_default_stream_clients_replayed_by_torch_on_the_device(monkeypatch):
+    """FKS_STREAM_MODE unset ("auto"): clients whose model sits on the GPU draw the
+    torch_rocm stream, the z an unmodified reference client on that GPU draws.  Two clients,
+    three rounds, the optimizer loop with the wire format (the records carry the stream
+    tag); each client's whole tensor replayed through the reference's own torch ops on the
+    device -- the reconstruct (fedkseed.py:130-141 into zo_utils.py:42-52), then every
+    local step (optimizer.py:108-173: perturb +eps, -2 eps, +eps with torch.normal on the
+    device, g from the synthetic closure, the update with the 0-dim g) -- bit for bit,
+    every g equal to the reference's, every history its steps'."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from harness import c5_round
+    from oracle import torch_replica as R
+    monkeypatch.setenv("FKS_STREAM_MODE", "auto")  # the spawned clients see it at import
+    rounds, k, steps, n = 3, 32, 4, 65536
+    out = c5_round.main(["--params", str(n), "--k", str(k), "--steps", str(steps), "--rounds", str(rounds),
+                         "--clients", "2", "--wire", "--placement", "pinned", "--record", "--record-prefix", "0"])
+    recs = out["client_records"]
+    dev = torch.device("cuda", 0)
+
+    def tensor(bits):
+        return torch.from_numpy(np.array(bits, dtype=np.uint16).view(np.int16)).view(torch.bfloat16).to(dev)
+
+    def perturb(p, seed, sf, eps=5e-4):  # optimizer.py:165-173
+        torch.manual_seed(seed)
+        z = torch.normal(mean=0, std=1, size=p.size(), device=p.device, dtype=p.dtype)
+        return p + sf * eps * z
+
+    def loss(p):  # harness SyntheticModel.forward
+        return p.view(-1)[:4096].float().square().mean() * 1e3
+
+    checked = 0
+    for c in sorted(recs):
+        model_0 = tensor(recs[c]["model_0"])
+        assert model_0.numel() == n
+        for r, rnd in enumerate(recs[c]["rounds"]):
+            p = [model_0.clone()]
+            if rnd["sums"]:
+                keep = [(int(s), v) for s, v in rnd["sums"].items() if v != 0.0]
+                R.reconstruct(p, [s for s, _ in keep], [v for _, v in keep], 1e-5, 0.0)
+            assert torch.equal(p[0].view(torch.int16), tensor(rnd["after_reconstruct"]).view(torch.int16)), (c, r)
+            hist = {}
+            for seed, g, lr in rnd["steps"]:
+                x = perturb(p[0], seed, 1.0)
+                right = loss(x)
+                x = perturb(x, seed, -2.0)
+                left = loss(x)
+                x = perturb(x, seed, 1.0)
+                g_ref = (right - left) / (2 * 5e-4)
+                assert float(g_ref) == g, (c, r, seed, float(g_ref), g)
+                torch.manual_seed(seed)  # zo_utils.py:42-52, group 0's lr and weight decay 0.0
+                z = torch.normal(mean=0, std=1, size=x.size(), device=x.device, dtype=x.dtype)
+                p[0] = x - lr * (g_ref * z + 0.0 * x)
+                hist.setdefault(seed, []).append(g)
+                checked += 1
+            assert torch.equal(p[0].view(torch.int16), tensor(rnd["after_steps"]).view(torch.int16)), (c, r)
+            h = {int(s): v for s, v in rnd["history"].items()}
+            assert {s: v for s, v in h.items() if v} == hist
+    assert checked == 2 * rounds * steps
+
+
 def _offline_probabilities(hists, seeds, rounds, k):
     from fate_llm.algo.fedkseed.fedkseed import FedKSeedTrainingArguments, Trainer
 
