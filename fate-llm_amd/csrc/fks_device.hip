@@ -947,6 +947,21 @@ __device__ __forceinline__ float radius_sqrt(float x) {
   s = __builtin_fma(__builtin_fma(-s, s, d), h, s);
   return x == 0.0f ? x : (float)s;
 }
+#elif defined(FKS_SQRT_INTFIX) && FKS_SQRT_INTFIX
+// (A/B) ocml's correctly rounded expansion restricted to this domain (x is +-0 or a normal
+// float in [1.19e-7, 33.3]: no rescaling, no class select), its two compare-selects
+// replaced by integer arithmetic on the residuals' bits: with vm = fma(-(s-1ulp), s, x) and
+// vp = fma(-(s+1ulp), s, x) (never -0: an exact zero sum rounds to +0), "vm <= 0" is
+// 1 - [vm > 0] and [v > 0] is the sign bit of -bits(v), so the root's bits are
+// bits(s) - 1 + [vp > 0] + [vm > 0]; x = +-0 keeps s (= x)
+__device__ __forceinline__ float radius_sqrt(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const uint32_t sm = __float_as_uint(s) - 1u, sp = __float_as_uint(s) + 1u;
+  const float vm = __fmaf_rn(-__uint_as_float(sm), s, x);
+  const float vp = __fmaf_rn(-__uint_as_float(sp), s, x);
+  const uint32_t r = sm + ((0u - __float_as_uint(vp)) >> 31) + ((0u - __float_as_uint(vm)) >> 31);
+  return x == 0.0f ? s : __uint_as_float(r);
+}
 #else
 __device__ __forceinline__ float radius_sqrt(float x) { return sqrtf(x); }
 #endif
