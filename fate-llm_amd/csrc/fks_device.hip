@@ -2865,56 +2865,6 @@ __device__ __forceinline__ void phx_vitem(const PhiloxArgs& a, const PhxTensor& 
   for (int i = 0; i < 4; i++) phx_store8<DT>(T.ptr, e0 + (int64_t)S * i, v[i]);
 }
 
-// FKS_PHX_VEC_PREFETCH (A/B): the next group's 16-byte runs (2-byte dtypes) are loaded
-// before this group's seed loop, so that a wave keeps its loads in flight while it computes
-#ifndef FKS_PHX_VEC_PREFETCH
-#define FKS_PHX_VEC_PREFETCH 0
-#endif
-template <int MODE>
-__device__ __forceinline__ bool phx_prefetch(const PhxTensor& T, int64_t r0, u32x4_t raw[4]) {
-  if (MODE == kModeWriteZ || T.dtype == FKS_F32 || kPhxVec != 8) return false;
-  const uint32_t S = T.stride;
-  const int64_t e0 = (int64_t)(uint32_t)(r0 % S) + (int64_t)S * (int64_t)(4 * (uint64_t)(r0 / S));
-  if (!(T.flags & kPhxP16) || e0 + 3 * (int64_t)S + kPhxVec > T.numel) return false;
-#pragma unroll
-  for (int i = 0; i < 4; i++) raw[i] = *reinterpret_cast<const gu128*>(T.ptr + (uint64_t)(e0 + (int64_t)S * i) * 2);
-  return true;
-}
-
-template <int DT, int MODE>
-__device__ __forceinline__ void phx_vitem_pre(const PhiloxArgs& a, const PhxTensor& T, int64_t r0,
-                                              const u32x4_t raw[4]) {
-  const uint32_t S = T.stride;
-  const uint32_t idx0 = (uint32_t)(r0 % S);
-  const uint64_t j = (uint64_t)(r0 / S);
-  const int64_t e0 = (int64_t)idx0 + (int64_t)S * (int64_t)(4 * j);
-  float v[4][kPhxVec];
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint32_t w[4] = {raw[i].x, raw[i].y, raw[i].z, raw[i].w};
-#pragma unroll
-    for (int c = 0; c < 4 && 2 * c + 1 < kPhxVec; c++) {
-      v[i][2 * c] = Traits<DT>::cvt(w[c] & 0xffffu);
-      v[i][2 * c + 1] = Traits<DT>::cvt(w[c] >> 16);
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < kPhxVec; q++) {
-    int64_t e[4];
-    float p[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      e[i] = e0 + (int64_t)S * i + q;
-      p[i] = v[i][q];
-    }
-    phx_seeds<DT, MODE>(a, T, idx0 + (uint32_t)q, j, e, p);
-#pragma unroll
-    for (int i = 0; i < 4; i++) v[i][q] = p[i];
-  }
-#pragma unroll
-  for (int i = 0; i < 4; i++) phx_store8<DT>(T.ptr, e0 + (int64_t)S * i, v[i]);
-}
-
 template <int MODE>
 __global__ __launch_bounds__(256) void fks_philox_kernel(PhiloxArgs a) {
   const int64_t step = (int64_t)gridDim.x * blockDim.x;
@@ -2942,15 +2892,6 @@ __global__ __launch_bounds__(256) void fks_philox_kernel(PhiloxArgs a) {
 #else
 #define FKS_PHX_VEC_ATTR
 #endif
-__device__ __forceinline__ int phx_find(const PhiloxArgs& a, int64_t it, int lo) {
-  int hi = a.nt - 1;  // the last tensor whose first item is <= it (items only grow)
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (a.t[mid].item0 <= it) lo = mid; else hi = mid - 1;
-  }
-  return lo;
-}
-
 // FKS_PHX_VEC_UNIFORM: the tensor of a wave's 64 groups is looked up once per wave, with
 // wave-uniform indices, instead of a per-lane binary search whose dependent vector loads
 // each wait for every load and store in flight (vmcnt is in order); 2 (default): from a
@@ -2993,48 +2934,10 @@ __device__ __forceinline__ void phx_vec_uniform(const PhiloxArgs& a, Tab tab, in
     it = w + (int64_t)lane * kPhxVec;
     return one ? t : phx_find_t(tab, a.nt, it < a.item_hi ? it : a.item_hi - 1, t, 0);
   };
-#if FKS_PHX_VEC_PREFETCH
-  u32x4_t raw[4];
-  bool pre = false;
-  if (wb < a.item_hi) {
-    ts = __builtin_amdgcn_readfirstlane(phx_find_t(tab, a.nt, wb, ts, 2));
-    int64_t it;
-    const int ti = lane_tensor(wb, ts, it);
-    if (it < a.item_hi) pre = phx_prefetch<MODE>(tab[ti], it - tab[ti].item0, raw);
-  }
-#endif
   for (; wb < a.item_hi; wb += step) {
     ts = __builtin_amdgcn_readfirstlane(phx_find_t(tab, a.nt, wb, ts, 2));
     int64_t it;
     const int ti = lane_tensor(wb, ts, it);
-#if FKS_PHX_VEC_PREFETCH
-    const PhxTensor T = tab[ti];  // (read before the prefetch: a global table read waits on vmcnt)
-    // the next groups' runs, loaded before this group's seed loop
-    u32x4_t nraw[4];
-    bool npre = false;
-    const int64_t nwb = wb + step;
-    if (nwb < a.item_hi) {
-      const int nts = __builtin_amdgcn_readfirstlane(phx_find_t(tab, a.nt, nwb, ts, 2));
-      int64_t nit;
-      const int nti = lane_tensor(nwb, nts, nit);
-      if (nit < a.item_hi) npre = phx_prefetch<MODE>(tab[nti], nit - tab[nti].item0, nraw);
-    }
-    if (it < a.item_hi) {
-      if (pre) {
-        if (T.dtype == FKS_BF16) phx_vitem_pre<FKS_BF16, MODE>(a, T, it - T.item0, raw);
-        else phx_vitem_pre<FKS_F16, MODE>(a, T, it - T.item0, raw);
-      } else {
-        switch (T.dtype) {
-          case FKS_F32: phx_vitem<FKS_F32, MODE>(a, T, it - T.item0); break;
-          case FKS_BF16: phx_vitem<FKS_BF16, MODE>(a, T, it - T.item0); break;
-          default: phx_vitem<FKS_F16, MODE>(a, T, it - T.item0); break;
-        }
-      }
-    }
-    pre = npre;
-#pragma unroll
-    for (int i = 0; i < 4; i++) raw[i] = nraw[i];
-#else
     if (it >= a.item_hi) continue;
     const PhxTensor T = tab[ti];
     switch (T.dtype) {
@@ -3042,7 +2945,6 @@ __device__ __forceinline__ void phx_vec_uniform(const PhiloxArgs& a, Tab tab, in
       case FKS_BF16: phx_vitem<FKS_BF16, MODE>(a, T, it - T.item0); break;
       default: phx_vitem<FKS_F16, MODE>(a, T, it - T.item0); break;
     }
-#endif
   }
 }
 
@@ -3062,39 +2964,6 @@ __global__ __launch_bounds__(256) FKS_PHX_VEC_ATTR void fks_philox_vec_kernel(Ph
   }
 #endif
   phx_vec_uniform<MODE>(a, a.t, step);
-#elif FKS_PHX_VEC_PREFETCH
-  int64_t it = a.item_lo + ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kPhxVec;
-  if (it >= a.item_hi) return;
-  int ti = phx_find(a, it, 0);
-  u32x4_t raw[4];
-  bool pre = phx_prefetch<MODE>(a.t[ti], it - a.t[ti].item0, raw);
-  while (true) {
-    const PhxTensor T = a.t[ti];
-    const int64_t nit = it + step;
-    int nti = ti;
-    u32x4_t nraw[4];
-    bool npre = false;
-    if (nit < a.item_hi) {
-      nti = phx_find(a, nit, ti);
-      npre = phx_prefetch<MODE>(a.t[nti], nit - a.t[nti].item0, nraw);
-    }
-    if (pre) {
-      if (T.dtype == FKS_BF16) phx_vitem_pre<FKS_BF16, MODE>(a, T, it - T.item0, raw);
-      else phx_vitem_pre<FKS_F16, MODE>(a, T, it - T.item0, raw);
-    } else {
-      switch (T.dtype) {
-        case FKS_F32: phx_vitem<FKS_F32, MODE>(a, T, it - T.item0); break;
-        case FKS_BF16: phx_vitem<FKS_BF16, MODE>(a, T, it - T.item0); break;
-        default: phx_vitem<FKS_F16, MODE>(a, T, it - T.item0); break;
-      }
-    }
-    if (nit >= a.item_hi) break;
-    it = nit;
-    ti = nti;
-    pre = npre;
-#pragma unroll
-    for (int i = 0; i < 4; i++) raw[i] = nraw[i];
-  }
 #else
   int t0 = 0;
   for (int64_t it = a.item_lo + ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kPhxVec; it < a.item_hi;
