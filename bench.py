@@ -130,26 +130,31 @@ def load_pmc_summary(wd=None, name=None):
         return {}
 
 
-def alt_stream_leg(codec, views, ks, kv, wd, total, build_id):
+def alt_stream_leg(codec, views, ks, kv, wd, total, build_id, steps):
     """The same 7B reconstruct drawn from the torch_rocm stream -- the z a reference client
-    draws when its model sits on an MI355X (zo_utils.py:47: device=param.data.device) --
-    timed once, with the VALU roofline of its kernel (fks_philox_vec_kernel)."""
+    draws when its model sits on an MI355X (zo_utils.py:47: device=param.data.device), and
+    the drop-in's DEFAULT stream on a GPU (codec "auto") -- timed over ``steps`` steps
+    (median reported), with the VALU roofline of its kernel (fks_philox_vec_kernel)."""
     specs = [codec.ParamSpec(v, lr=1e-5, weight_decay=wd) for v in views]
     codec.directional_step(specs, ks[:32], kv[:32], stream_mode="torch_rocm")  # the tensor table
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    times = []
     with codec.profile() as prof:
-        codec.directional_step(specs, ks, kv, stream_mode="torch_rocm")
-        torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    out = {"stream": "torch_rocm", "kernel": "fks_philox_vec_kernel", "weight_decay": wd, "steps": 1,
-           "ms_per_step": round(dt * 1e3, 1), "value": round(total * 2 / dt / 1e9, 4), "unit": "GB/s",
+        for _ in range(steps):
+            t0 = time.perf_counter()
+            codec.directional_step(specs, ks, kv, stream_mode="torch_rocm")
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+    dt = sorted(times)[len(times) // 2]
+    out = {"stream": "torch_rocm", "default_stream": True, "kernel": "fks_philox_vec_kernel", "weight_decay": wd,
+           "steps": steps, "ms_per_step": round(dt * 1e3, 1), "ms_per_step_all": [round(t * 1e3, 1) for t in times],
+           "value": round(total * 2 / dt / 1e9, 4), "unit": "GB/s",
            "ms_per_seed": round(dt * 1e3 / len(ks), 3), "launches": prof.n_apply,
-           "kernel_ms": round(prof.apply_ms, 1)}
+           "kernel_ms_per_step": round(prof.apply_ms / steps, 1)}
     pmc = load_pmc_summary(name=PMC_SUMMARY_PHX)
     lane_ops = pmc.get("valu_lane_ops_per_seed_param")
     if lane_ops and pmc.get("build_id") == build_id and wd == 0.0:
-        ach = total * len(ks) * lane_ops / (prof.apply_ms / 1e3) / 1e12
+        ach = total * len(ks) * steps * lane_ops / (prof.apply_ms / 1e3) / 1e12
         out["roofline"] = {"bound": "valu", "achieved": round(ach, 3), "peak": round(VALU_PEAK_TLANEOPS, 2),
                            "unit": "Tlane-op/s", "frac": round(ach / VALU_PEAK_TLANEOPS, 4),
                            "lane_ops_per_unit": round(lane_ops, 3), "build_id": build_id,
@@ -160,6 +165,29 @@ def alt_stream_leg(codec, views, ks, kv, wd, total, build_id):
         out["roofline_withheld"] = (f"profiles/{PMC_SUMMARY_PHX}: build {pmc.get('build_id')} / wd 0.0 only, "
                                     f"this run build {build_id} wd {wd}")
     return out
+
+
+def hd_leg(codec, flat, specs, ks, kv, stream, host):
+    """The north star's path from host memory to host memory: model_0 host -> device (the
+    reference's .to(device), fedkseed.py:133, from pinned memory), the reconstruct, and the
+    result back to the host (its state dict), timed end to end on one stream, once."""
+    sync = torch.cuda.synchronize
+    sync()
+    t0 = time.perf_counter()
+    flat.copy_(host, non_blocking=True)
+    sync()
+    t1 = time.perf_counter()
+    codec.directional_step(specs, ks, kv, stream_mode=stream)
+    sync()
+    t2 = time.perf_counter()
+    host.copy_(flat, non_blocking=True)
+    sync()
+    t3 = time.perf_counter()
+    nbytes = flat.numel() * flat.element_size()
+    return {"stream": stream, "h2d_ms": round((t1 - t0) * 1e3, 1), "reconstruct_ms": round((t2 - t1) * 1e3, 1),
+            "d2h_ms": round((t3 - t2) * 1e3, 1), "total_ms": round((t3 - t0) * 1e3, 1),
+            "value": round(nbytes / (t3 - t0) / 1e9, 4), "unit": "GB/s",
+            "h2d_GBps": round(nbytes / (t1 - t0) / 1e9, 1), "d2h_GBps": round(nbytes / (t3 - t2) / 1e9, 1)}
 
 
 # ------------------------------------------------------------------ CPU baseline
@@ -424,7 +452,15 @@ def run(args, world, rank, local):
     build_id = _native.build_id()
     alt_stream = None
     if world == 1 and not seed_shard and args.alt_stream == "torch_rocm":
-        alt_stream = alt_stream_leg(codec, views, ks, kv, wd, total, build_id)
+        alt_stream = alt_stream_leg(codec, views, ks, kv, wd, total, build_id, max(1, args.alt_stream_steps))
+
+    hd = None
+    if world == 1 and not seed_shard and args.hd:
+        # PCIe-inclusive rate for both streams (reported beside value, never as it)
+        host = torch.empty(total, dtype=dtype, pin_memory=True)
+        host.copy_(flat)
+        hd = {s: hd_leg(codec, flat, specs, ks, kv, s, host) for s in ("torch_cpu", "torch_rocm")}
+        del host
 
     ms_per_step = dt / args.steps * 1e3
     buf_bytes = total * 2 * (world if weak else 1)  # weak: one buffer per rank
@@ -508,6 +544,9 @@ def run(args, world, rank, local):
                    f"{world}xMI355X: 7B-param bf16 buffer, K=4096 seeds, element-sharded (bit-exact, no collective)",
                    "params": total, "k": args.k, "k_nonzero": len(ks), "tensors": len(shapes),
                    "lr": 1e-5, "weight_decay": wd, "stream": "torch_cpu",
+                   "stream_note": ("value draws torch's CPU-generator stream (the oracle-pinned one; a reference "
+                                   "client training on the CPU, FKS_STREAM_MODE=torch_cpu); the drop-in's default "
+                                   "on a GPU ('auto') draws torch_rocm, timed as alt_stream"),
                    "parallelism": (f"seed-shard{world}" if seed_shard else
                                    f"client-per-gpu{world}" if weak else f"element-shard{world}")},
         "roofline": valu if valu else hbm,
@@ -527,6 +566,8 @@ def run(args, world, rank, local):
         out["alt_weight_decay"] = alt
     if alt_stream is not None:
         out["alt_stream"] = alt_stream
+    if hd is not None:
+        out["hd_inclusive"] = hd
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_budget, wd)
     if rank == 0:
@@ -551,6 +592,9 @@ def main():
     ap.add_argument("--alt-stream", choices=("torch_rocm", "none"), default="torch_rocm",
                     help="N = 1: one more timed reconstruct drawing the torch_rocm stream (a reference client "
                          "whose model sits on the GPU), with its kernel's VALU roofline")
+    ap.add_argument("--alt-stream-steps", type=int, default=3, help="timed steps of the torch_rocm leg (median)")
+    ap.add_argument("--no-hd", dest="hd", action="store_false",
+                    help="N = 1: skip the host -> device -> host legs (H2D + reconstruct + D2H, both streams)")
     ap.add_argument("--cpu-budget", type=float, default=24.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("sequential", "seed-shard"), default="sequential")

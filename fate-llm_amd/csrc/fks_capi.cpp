@@ -41,6 +41,10 @@ struct Layout {
   // buffer (element e of tensor i at delta[cum_numel(i) + e]) instead of the parameters;
   // the dtype still selects the z generator
   bool delta = false;
+  // the generator after the list's draws: CPUGeneratorImpl::next_double_normal_sample holds
+  // the second value of the Box-Muller pair at stream word end_pair (fks_cpu_generator_end)
+  bool end_cached = false;
+  int64_t end_pair = 0;
 };
 
 inline size_t elem_size(int dtype) { return dtype == FKS_F32 ? 4 : 2; }
@@ -135,6 +139,8 @@ Layout make_layout(const fks_tensor* t, int nt, const double* scales = nullptr, 
     }
   }
   L.stream_len = pos;
+  L.end_cached = cached;
+  L.end_pair = cached_pair;
   // runs are disjoint and already in stream order; single elements sorted by the
   // block holding their last word, the order the kernel walks them in
   std::vector<size_t> order(L.tiny.size());
@@ -734,7 +740,9 @@ struct PhxPlan {
   float max_lr = 0.0f;         // max |lr| over the table (the WdPos0 bound)
   std::vector<PhxTensor> tab;  // host copy of the table
   std::vector<int64_t> elem0;  // per entry: its first element in the concatenation of ALL the call's tensors
+  std::vector<int> tensor_of;  // per entry: the tensor it belongs to (a tensor past 2^31 bytes has several)
   int64_t elems = 0;           // elements of all the call's tensors
+  uint64_t off4_total = 0;     // the Philox offset / 4 one seed's draws advance the generator by
 };
 std::vector<PhxPlan*> g_phx;
 
@@ -956,40 +964,71 @@ int jump_chunks_per_wg(int nseeds, int nchunks) {
 // The table and geometry alone, on the host (nothing cached, nothing uploaded): what
 // fks_shard_census reads; get_phx_plan adds the device copy.  Needs a current device
 // (its CU count and threads per CU set torch's grid).
-void phx_geometry(const fks_tensor* t, int nt, const double* scales, PhxPlan* P) {
+// torch's TensorIteratorBase::can_use_32bit_indexing for a contiguous 1-D draw of m elements of
+// es bytes: numel and the largest byte offset + 1 both within INT32_MAX
+inline bool phx_fits32(int64_t m, size_t es) {
+  return m <= (int64_t)INT32_MAX && 1 + (m - 1) * (int64_t)es <= (int64_t)INT32_MAX;
+}
+// calc_execution_policy (DistributionTemplates.h:50-62) for m elements: (stride, loop iterations)
+inline void phx_policy(int64_t m, int64_t max_grid, int64_t& stride, int64_t& J) {
+  const uint32_t grid0 = (uint32_t)(((uint64_t)m + 255u) / 256u);  // dim3 grid((numel + 255) / 256)
+  const int64_t grid = std::min<int64_t>(grid0, max_grid);
+  stride = 256 * grid;
+  J = (m - 1) / (4 * stride) + 1;  // counter_offset / 4
+}
+
+void phx_geometry(const fks_tensor* t, int nt, const double* scales, PhxPlan* P, uint64_t delta_base) {
   const int64_t max_grid = (int64_t)device_cu_count() * (device_max_threads_per_cu() / 256);
   std::vector<PhxTensor> tab;
   std::vector<int64_t> elem0;
+  std::vector<int> tensor_of;
   uint64_t off4 = 0;
   int64_t items = 0, elems = 0;
   for (int i = 0; i < nt; i++) {
     const int64_t n = t[i].numel;
     elems += n;
     if (n == 0) continue;  // torch draws nothing for an empty tensor (the offset stays)
-    if (n * (int64_t)elem_size(t[i].dtype) > (int64_t)INT32_MAX)
-      throw Error(-FKS_ENOTSUP, "tensor " + std::to_string(i) +
-                                    ": torch_rocm stream of a tensor past 2^31 bytes (torch splits its draw) is not supported");
-    const int64_t grid = std::min<int64_t>((n + 255) / 256, max_grid);
-    const int64_t stride = 256 * grid;
-    const int64_t J = (n - 1) / (4 * stride) + 1;  // loop iterations = philox offset increment / 4
-    if (!(t[i].flags & FKS_FROZEN)) {
+    const size_t es = elem_size(t[i].dtype);
+    const bool live = !(t[i].flags & FKS_FROZEN);
+    const uint64_t base = delta_base ? delta_base + 4 * (uint64_t)(elems - n) : (uint64_t)(uintptr_t)t[i].data;
+    const size_t ses = delta_base ? 4 : es;  // bytes per stored element
+    // distribution_nullary_kernel (DistributionTemplates.h:111-133): the draw of m elements
+    // first reserves its own offset increment, then -- when the iterator cannot use 32-bit
+    // indexing -- draws the two halves TensorIterator::with_32bit_indexing splits it into
+    // (first floor(m / 2) elements, then the rest, recursively), each reserving its own.
+    // A piece is a table entry of its own (its elements, stride and offset).
+    auto draw = [&](auto&& self, int64_t start, int64_t m) -> void {
+      int64_t stride = 0, J = 0;
+      phx_policy(m, max_grid, stride, J);
+      const uint64_t my_off4 = off4;
+      off4 += (uint64_t)J;
+      if (!phx_fits32(m, es)) {
+        const int64_t h = m / 2;
+        self(self, start, h);
+        self(self, start + h, m - h);
+        return;
+      }
+      if (!live) return;
       PhxTensor x{};
-      x.ptr = (uint64_t)(uintptr_t)t[i].data;
-      x.numel = n;
+      x.ptr = base + (uint64_t)start * ses;
+      x.numel = m;
       x.item0 = items;
-      x.off4 = off4;
+      x.off4 = my_off4;
       x.stride = (uint32_t)stride;
       x.dtype = t[i].dtype;
       x.lr = t[i].lr;
       x.wd = t[i].wd;
-      x.flags = (t[i].flags & FKS_HAS_WD) | (((uintptr_t)t[i].data % 16u) == 0 ? kPhxP16 : 0u);
+      x.flags = (t[i].flags & FKS_HAS_WD) | ((x.ptr % 16u) == 0 ? kPhxP16 : 0u);
       x.ps = scales ? (float)scales[i] : 0.0f;
       tab.push_back(x);
-      elem0.push_back(elems - n);
+      elem0.push_back(elems - n + start);
+      tensor_of.push_back(i);
       items += stride * J;
-    }
-    off4 += (uint64_t)J;
+    };
+    draw(draw, 0, n);
   }
+  P->off4_total = off4;
+  P->tensor_of = std::move(tensor_of);
   P->nt = (int)tab.size();
   P->items = items;
   P->elems = elems;
@@ -1015,8 +1054,8 @@ void phx_geometry(const fks_tensor* t, int nt, const double* scales, PhxPlan* P)
   P->elem0 = std::move(elem0);
 }
 
-PhxPlan* get_phx_plan(const fks_tensor* t, int nt, const double* scales) {
-  std::vector<uint8_t> key = plan_key(t, nt, scales, 0, 0, 1, false);
+PhxPlan* get_phx_plan(const fks_tensor* t, int nt, const double* scales, uint64_t delta_base = 0) {
+  std::vector<uint8_t> key = plan_key(t, nt, scales, delta_base, 0, 1, false);
   key_put(key, (int)0x7068);  // "ph": not an MT plan key
   key_put(key, device_max_threads_per_cu());
   const uint64_t h = fnv1a(key);
@@ -1027,7 +1066,7 @@ PhxPlan* get_phx_plan(const fks_tensor* t, int nt, const double* scales) {
     }
   auto* P = new PhxPlan();
   try {
-    phx_geometry(t, nt, scales, P);
+    phx_geometry(t, nt, scales, P, delta_base);
   } catch (...) {
     delete P;
     throw;
@@ -1089,11 +1128,13 @@ int64_t phx_boundary_elem(const PhxPlan* P, int64_t b) {
 // the torch_rocm stream: seeds in passes of kPhxSeeds (by value in the kernel arguments);
 // element shards split the work items
 void run_philox(const fks_tensor* t, int nt, const uint64_t* seeds, const double* values, int k, int value_kind,
-                int mode, void* stream, const double* scales, int shard, int nshards, const float* gdev) {
-  if (mode != kModeUpdate && mode != kModePerturb && mode != kModePerturbUpdate && mode != kModeWriteZ)
-    throw Error(-FKS_ENOTSUP, "the torch_rocm stream supports the reconstruct, perturb and normal calls only");
+                int mode, void* stream, const double* scales, int shard, int nshards, const float* gdev,
+                uint64_t delta_base) {
+  if (mode != kModeUpdate && mode != kModePerturb && mode != kModePerturbUpdate && mode != kModeWriteZ &&
+      mode != kModeDelta)
+    throw Error(-FKS_ENOTSUP, "the torch_rocm stream supports the reconstruct, perturb, normal and delta calls only");
   std::lock_guard<std::mutex> lk(g_cache_mu);
-  const PhxPlan* P = get_phx_plan(t, nt, scales);
+  const PhxPlan* P = get_phx_plan(t, nt, scales, mode == kModeDelta ? delta_base : 0);
   if (P->nt == 0 || P->items == 0) return;
   PhiloxArgs a{};
   a.t = static_cast<const PhxTensor*>(P->dev);
@@ -1141,7 +1182,7 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
     throw Error(-FKS_EINVAL, "bad value_kind");
   if (k == 0 || nt == 0) return;
   if (rocm_stream(t, nt)) {
-    run_philox(t, nt, seeds, values, k, value_kind, mode, stream, tensor_scales, shard, nshards, gdev);
+    run_philox(t, nt, seeds, values, k, value_kind, mode, stream, tensor_scales, shard, nshards, gdev, delta_base);
     return;
   }
   const bool small = k <= kSmallK;
@@ -1577,6 +1618,65 @@ int fks_stream_length(const fks_tensor* t, int32_t nt, int64_t* words) {
   });
 }
 
+int fks_cpu_generator_end(const fks_tensor* t, int32_t nt, uint64_t seed, uint32_t* state624, int32_t* left,
+                          uint32_t* next, int32_t* normal_valid, double* normal) {
+  return guarded([&] {
+    validate(t, nt);
+    if (!state624 || !left || !next || !normal_valid || !normal) throw Error(-FKS_EINVAL, "null output");
+    const Layout L = make_layout(t, nt);
+    const int64_t W = L.stream_len;
+    // at::mt19937::operator() (MT19937RNGEngine.h): a word first decrements left_ and twists
+    // the whole state when it reaches 0 (left_ = 624, next_ = 0), then returns state_[next_++];
+    // manual_seed leaves left_ = 1, next_ = 0.  After W >= 1 words the state has been twisted
+    // ceil(W / 624) times -- the untempered words x[624 t, 624 t + 624) -- and next_ words of it used.
+    const int64_t tw = (W + 623) / 624;
+    host_jump_window(seed, tw, state624);
+    *next = W ? (uint32_t)(W - 624 * (tw - 1)) : 0u;
+    *left = W ? 625 - (int32_t)*next : 1;
+    *normal_valid = 0;
+    *normal = 0.0;
+    if (L.end_cached) {  // normal_distribution<double> (DistributionsHelper.h:189-221): r sin(theta) cached
+      uint32_t w[4];
+      host_x_words(seed, 624 + L.end_pair, 4, w);  // output word k is temper(x[624 + k])
+      for (uint32_t& y : w) {
+        y ^= (y >> 11);
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= (y >> 18);
+      }
+      // random64() = (first word << 32) | second; uniform_real_distribution<double>: 53 bits
+      const uint64_t m53 = (1ull << 53) - 1;
+      const double u1 = (double)((((uint64_t)w[0] << 32) | w[1]) & m53) * (1.0 / 9007199254740992.0);
+      const double u2 = (double)((((uint64_t)w[2] << 32) | w[3]) & m53) * (1.0 / 9007199254740992.0);
+      const double r = std::sqrt(-2.0 * std::log1p(-u2));
+      const double theta = 2.0 * 3.14159265358979323846 * u1;
+      *normal = r * std::sin(theta);
+      *normal_valid = 1;
+    }
+  });
+}
+
+int fks_rocm_grid_cap(int64_t* blocks) {
+  return guarded([&] {
+    int dev = 0;
+    if (!blocks) throw Error(-FKS_EINVAL, "null output");
+    if (hipGetDevice(&dev) != hipSuccess) throw Error(-FKS_EHIP, "no current HIP device");
+    *blocks = (int64_t)device_cu_count() * (device_max_threads_per_cu() / 256);
+  });
+}
+
+int fks_rocm_offset(const fks_tensor* t, int32_t nt, uint64_t* offset) {
+  return guarded([&] {
+    validate(t, nt);
+    if (!offset) throw Error(-FKS_EINVAL, "null output");
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) throw Error(-FKS_EHIP, "no current HIP device");
+    PhxPlan geo;
+    phx_geometry(t, nt, nullptr, &geo, 0);
+    *offset = 4 * geo.off4_total;
+  });
+}
+
 int fks_shard_census(const fks_tensor* t, int32_t nt, int32_t shard, int32_t nshards, int64_t* word_range,
                      int64_t* written) {
   return guarded([&] {
@@ -1586,7 +1686,7 @@ int fks_shard_census(const fks_tensor* t, int32_t nt, int32_t shard, int32_t nsh
       // host geometry only: no plan cache entry, no device allocation (the scales do not
       // move row boundaries)
       PhxPlan geo;
-      phx_geometry(t, nt, nullptr, &geo);
+      phx_geometry(t, nt, nullptr, &geo, 0);
       const PhxPlan* P = &geo;
       const int64_t lo = phx_boundary(P, shard, nshards), hi = phx_boundary(P, shard + 1, nshards);
       if (word_range) {
@@ -1595,15 +1695,12 @@ int fks_shard_census(const fks_tensor* t, int32_t nt, int32_t shard, int32_t nsh
       }
       if (!written) return;
       for (int i = 0; i < nt; i++) written[i] = 0;
-      int ti = 0;  // table entry -> tensor index: the non-empty, non-frozen tensors in order
-      for (int k = 0; k < P->nt; k++) {
-        while (t[ti].numel == 0 || (t[ti].flags & FKS_FROZEN)) ti++;
+      for (int k = 0; k < P->nt; k++) {  // table entries: the pieces of the non-empty, non-frozen tensors
         const PhxTensor& T = P->tab[k];
         const int64_t a0 = std::max(lo, T.item0), a1 = std::min(hi, T.item0 + T.stride * ((T.numel - 1) / (4 * (int64_t)T.stride) + 1));
         if (a1 > a0)
-          written[ti] = std::min<int64_t>(T.numel, 4 * ((a1 - T.item0) / T.stride) * (int64_t)T.stride) -
-                        std::min<int64_t>(T.numel, 4 * ((a0 - T.item0) / T.stride) * (int64_t)T.stride);
-        ti++;
+          written[P->tensor_of[k]] += std::min<int64_t>(T.numel, 4 * ((a1 - T.item0) / T.stride) * (int64_t)T.stride) -
+                                      std::min<int64_t>(T.numel, 4 * ((a0 - T.item0) / T.stride) * (int64_t)T.stride);
       }
       return;
     }

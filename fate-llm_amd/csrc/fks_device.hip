@@ -2722,7 +2722,7 @@ __device__ __forceinline__ void phx_seeds(const PhiloxArgs& a, const PhxTensor& 
     if (MODE == kModeWriteZ) {
       pA = zA;
       pB = zB;
-    } else if constexpr (DT == FKS_F16) {  // torch's device rounding of the products (mul_f16_ref)
+    } else if constexpr (DT == FKS_F16 && MODE != kModeDelta) {  // torch's device rounding of the products (mul_f16_ref)
       // wd p at the call's first seed reads the caller's parameter (its alignment); later
       // seeds read the reference's freshly allocated, aligned result.  (kModePerturbUpdate's
       // update follows the restore perturbation, whose result is fresh.)
@@ -2742,7 +2742,7 @@ __device__ __forceinline__ void phx_seeds(const PhiloxArgs& a, const PhxTensor& 
 
 template <int DT, int MODE>
 __device__ __forceinline__ void phx_item(const PhiloxArgs& a, const PhxTensor& T, int64_t r) {
-  using TR = Traits<DT>;
+  using TR = Traits<MODE == kModeDelta ? FKS_F32 : DT>;  // storage (kModeDelta: the f32 delta)
   const uint32_t S = T.stride;
   const uint32_t idx = (uint32_t)(r % S);
   const uint64_t j = (uint64_t)(r / S);
@@ -2828,6 +2828,7 @@ __device__ __forceinline__ void phx_store8(uint64_t ptr, int64_t e, const float 
 
 template <int DT, int MODE>
 __device__ __forceinline__ void phx_vitem(const PhiloxArgs& a, const PhxTensor& T, int64_t r0) {
+  constexpr int ST = MODE == kModeDelta ? FKS_F32 : DT;  // storage (kModeDelta: the f32 delta)
   const uint32_t S = T.stride;
   const uint32_t idx0 = (uint32_t)(r0 % S);
   const uint64_t j = (uint64_t)(r0 / S);
@@ -2845,7 +2846,7 @@ __device__ __forceinline__ void phx_vitem(const PhiloxArgs& a, const PhxTensor& 
 #pragma unroll
       for (int q = 0; q < kPhxVec; q++) v[i][q] = 0.0f;
     } else {
-      phx_load8<DT>(T.ptr, e0 + (int64_t)S * i, v[i]);
+      phx_load8<ST>(T.ptr, e0 + (int64_t)S * i, v[i]);
     }
   }
 #pragma unroll
@@ -2862,7 +2863,7 @@ __device__ __forceinline__ void phx_vitem(const PhiloxArgs& a, const PhxTensor& 
     for (int i = 0; i < 4; i++) v[i][q] = p[i];
   }
 #pragma unroll
-  for (int i = 0; i < 4; i++) phx_store8<DT>(T.ptr, e0 + (int64_t)S * i, v[i]);
+  for (int i = 0; i < 4; i++) phx_store8<ST>(T.ptr, e0 + (int64_t)S * i, v[i]);
 }
 
 template <int MODE>
@@ -3339,6 +3340,7 @@ int launch_philox(const PhiloxArgs& a, void* stream) {
     case kModePerturb: return launch_philox_m<kModePerturb>(a, stream);
     case kModePerturbUpdate: return launch_philox_m<kModePerturbUpdate>(a, stream);
     case kModeWriteZ: return launch_philox_m<kModeWriteZ>(a, stream);
+    case kModeDelta: return launch_philox_m<kModeDelta>(a, stream);
     default: return -FKS_ENOTSUP;
   }
 }

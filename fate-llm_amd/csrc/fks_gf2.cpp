@@ -251,9 +251,12 @@ void jump_polys_for_blocks(const std::vector<int64_t>& blocks, std::vector<uint6
   }
 }
 
-// CPU evaluation of the jump (tests only): window of x at 624*block for `seed`.
+// CPU evaluation of the jump: window of x at 624*block for `seed` (the generator state
+// after `block` twists).  The self checks compare it with the oracle; fks_cpu_generator_end
+// uses it to leave torch's CPU generator where the reference leaves it.  One pass over the
+// set coefficients of c (about 10^4), each xoring 624 consecutive words into the window.
 void host_jump_window(uint64_t seed, int64_t block, uint32_t* out624) {
-  std::vector<uint32_t> x(624 * 34 + 16);
+  std::vector<uint32_t> x(624 + kDeg + 16);
   x[0] = (uint32_t)(seed & 0xffffffffu);
   for (int j = 1; j < 624; j++) x[j] = 1812433253u * (x[j - 1] ^ (x[j - 1] >> 30)) + (uint32_t)j;
   for (size_t n = 624; n < x.size(); n++) {
@@ -266,12 +269,29 @@ void host_jump_window(uint64_t seed, int64_t block, uint32_t* out624) {
   }
   std::vector<uint64_t> c;
   jump_polys_for_blocks({block}, c);
-  for (int w = 0; w < 624; w++) {
-    uint32_t acc = 0;
-    for (int i = 0; i < kDeg; i++)
-      if ((c[(size_t)i >> 6] >> (i & 63)) & 1u) acc ^= x[(size_t)i + w + 1];  // y[i+w] = x[i+w+1]
-    out624[w] = acc;
+  uint32_t acc[624] = {};
+  for (int wi = 0; wi < kWords; wi++) {
+    for (uint64_t bits = c[(size_t)wi]; bits; bits &= bits - 1) {
+      const int i = 64 * wi + __builtin_ctzll(bits);
+      if (i >= kDeg) break;
+      const uint32_t* src = x.data() + i + 1;  // y[i + w] = x[i + w + 1]
+      for (int w = 0; w < 624; w++) acc[w] ^= src[w];
+    }
   }
+  std::memcpy(out624, acc, sizeof(acc));
+}
+
+// x[first .. first + n) of `seed` (untempered words; x[0..623] = the seeded state): the
+// jumped window of the block holding `first`, extended by the recurrence.
+void host_x_words(uint64_t seed, int64_t first, int n, uint32_t* out) {
+  const int64_t block = first / 624;
+  std::vector<uint32_t> x((size_t)(624 + (first - 624 * block) + n + 624));
+  host_jump_window(seed, block, x.data());
+  for (size_t k = 624; k < x.size(); k++) {
+    const uint32_t u = x[k - 624], v = x[k - 623];
+    x[k] = x[k - 227] ^ ((((u & 0x80000000u) | (v & 0x7fffffffu)) >> 1) ^ ((v & 1u) ? 0x9908b0dfu : 0u));
+  }
+  std::memcpy(out, x.data() + (first - 624 * block), sizeof(uint32_t) * (size_t)n);
 }
 
 const std::vector<uint64_t>& charpoly() { return field().phi; }

@@ -27,6 +27,7 @@ constexpr uint32_t kMatrixA = 0x9908b0dfu;
 int jump_poly_words();  // 312
 void jump_polys_for_blocks(const std::vector<int64_t>& blocks, std::vector<uint64_t>& out);
 void host_jump_window(uint64_t seed, int64_t block, uint32_t* out624);
+void host_x_words(uint64_t seed, int64_t first, int n, uint32_t* out);  // untempered x[first, first + n)
 
 // ---- Box-Muller tables for the 8-bit (bf16) and 11-bit (f16) uniforms (fks_tables.cpp) ----
 // radius[a], cos[b], sin[b] as float values of the reduced type, exactly as

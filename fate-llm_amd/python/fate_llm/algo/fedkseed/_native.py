@@ -29,7 +29,7 @@ EXPORTED = (
     "fks_shard_census", "fks_perturb_step", "fks_delta_workspace_size", "fks_delta_accumulate", "fks_delta_apply",
     "fks_plan_cache_clear", "fks_perturb_step_dev", "fks_device_selfcheck", "fks_build_id",
     "fks_zindex_size", "fks_zindex_attach", "fks_jwin_size", "fks_jwin_size_shard", "fks_jwin_attach",
-    "fks_jwin_stats",
+    "fks_jwin_stats", "fks_cpu_generator_end", "fks_rocm_offset", "fks_rocm_grid_cap",
 )
 
 
@@ -95,12 +95,17 @@ def load():
         L.fks_jwin_size_shard.argtypes = [P, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_sz)]
         L.fks_jwin_attach.argtypes = [P, c_sz]
         L.fks_jwin_stats.argtypes = [ctypes.POINTER(c_u64), ctypes.POINTER(c_u64)]
+        L.fks_cpu_generator_end.argtypes = [P, c_i32, c_u64, P, ctypes.POINTER(c_i32), ctypes.POINTER(ctypes.c_uint32),
+                                            ctypes.POINTER(c_i32), ctypes.POINTER(ctypes.c_double)]
+        L.fks_rocm_offset.argtypes = [P, c_i32, ctypes.POINTER(c_u64)]
+        L.fks_rocm_grid_cap.argtypes = [ctypes.POINTER(ctypes.c_int64)]
         for name in ("fks_workspace_size", "fks_directional_step", "fks_perturb", "fks_normal",
                      "fks_host_jump_window", "fks_host_tables", "fks_directional_step_shard",
                      "fks_stream_length", "fks_profile_begin", "fks_profile_end", "fks_shard_census", "fks_perturb_step",
                      "fks_delta_workspace_size", "fks_delta_accumulate", "fks_delta_apply", "fks_plan_cache_clear",
                      "fks_perturb_step_dev", "fks_device_selfcheck", "fks_zindex_size", "fks_zindex_attach",
-                     "fks_jwin_size", "fks_jwin_size_shard", "fks_jwin_attach", "fks_jwin_stats"):
+                     "fks_jwin_size", "fks_jwin_size_shard", "fks_jwin_attach", "fks_jwin_stats",
+                     "fks_cpu_generator_end", "fks_rocm_offset", "fks_rocm_grid_cap"):
             getattr(L, name).restype = ctypes.c_int
         if L.fks_abi_version() != ABI_VERSION:
             raise OSError(f"libfks.so ABI {L.fks_abi_version()} != {ABI_VERSION}")

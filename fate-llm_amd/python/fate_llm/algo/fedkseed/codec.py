@@ -14,10 +14,11 @@ Three operations, each replacing one reference routine (include/fks.h has the AB
 The z stream (``stream_mode``) is the one the reference draws where its parameters live
 (zo_utils.py:47 and optimizer.py:170-172 draw on ``param.data.device``):
 
-* ``"torch_cpu"`` (default): torch's CPU generator, mt19937 + normal_fill -- a reference
-  client that trains on the CPU (the FedKSeed tutorial's configuration);
 * ``"torch_rocm"``: torch's HIP-device generator, Philox4x32-10 + rocrand's Box-Muller in
-  torch's grid-stride mapping -- a reference client whose model sits on an MI355X.
+  torch's grid-stride mapping -- a reference client whose model sits on an MI355X, and
+  what the default ``"auto"`` resolves to for every tensor the codec accepts;
+* ``"torch_cpu"``: torch's CPU generator, mt19937 + normal_fill -- a reference client that
+  trains on the CPU (the FedKSeed tutorial's configuration); an explicit choice.
 
 All parties of one federation must draw the same stream.  The
 process-wide setting comes from ``FKS_STREAM_MODE`` and ``set_stream_mode``: one of the
@@ -28,7 +29,8 @@ an unmodified reference client on the same device gives.  ``torch_cpu`` (1.8x fa
 here) is the explicit choice for a federation whose reference clients train on the CPU,
 or whose parties are all drop-in clients; the round payloads carry the stream so that a
 drop-in arbiter rejects a mixed federation (payload.py).  Updates are applied in
-place (the reference rebinds ``param.data`` to a new tensor of identical values).
+place (the reference rebinds ``param.data`` to a new tensor of identical values), and
+torch's generators are left where the reference's draws leave them (``_leave``).
 
 There is no CPU path: tensors must live on a HIP device and libfks.so must be
 loadable, otherwise these functions raise.
@@ -164,16 +166,107 @@ def _seed_u64(s) -> int:
     return s
 
 
+# ---------------------------------------------------------------- torch's global generators
+# The reference draws z from torch's generators right after torch.manual_seed(seed)
+# (zo_utils.py:42,47; optimizer.py:165,170-172), so once a call returns, the generator of
+# the parameters' device stands past the last seed's draws, and whatever the caller draws
+# next -- a sampler's permutation, the dropout of the zeroth-order closure -- starts there.
+# The codec's kernels draw nothing from torch; every call that stands for the reference's
+# draws (leave_generator=True, the default) re-seeds torch with the last seed and moves the
+# generator of the call's stream to where the reference's draws leave it:
+#   torch_rocm: the device generator's Philox offset (fks_rocm_offset);
+#   torch_cpu:  the CPU generator's mt19937 state and its cached normal (fks_cpu_generator_end).
+_CPU_STATE_BYTES = 5056  # sizeof(CPUGeneratorImplState) (ATen/CPUGeneratorImpl.h), torch.get_rng_state()
+_cpu_state_cache = {}    # (numels, seed) -> state tensor: the zeroth-order step's three calls share one
+_cpu_state_lock = threading.Lock()
+
+
+def cpu_generator_state(arr, n: int, seed: int) -> torch.Tensor:
+    """The CPU generator's state (torch.get_rng_state() bytes) after torch.manual_seed(seed)
+    and the CPU-stream draws of the ``n`` fks_tensor entries of ``arr`` (host-only: only
+    their sizes and dtypes matter): CPUGeneratorImplState = the legacy THGeneratorState
+    (the_initial_seed u64 @0, left i32 @8, seeded i32 @12, next u64 @16, state u64[624]
+    @24, normal_x / normal_y / normal_rho f64 @5016 / 5024 / 5032, normal_is_valid i32
+    @5040) + the float normal cache @5048 (reset by manual_seed)."""
+    seed = _seed_u64(seed)
+    key = (tuple((int(x.numel), int(x.dtype)) for x in arr[:n]), seed)
+    with _cpu_state_lock:
+        hit = _cpu_state_cache.get(key)
+    if hit is not None:
+        return hit
+    st = np.zeros(624, dtype=np.uint32)
+    left, nxt = ctypes.c_int32(0), ctypes.c_uint32(0)
+    valid, normal = ctypes.c_int32(0), ctypes.c_double(0.0)
+    N.check(N.load().fks_cpu_generator_end(ctypes.addressof(arr), n, seed, st.ctypes.data, ctypes.byref(left),
+                                           ctypes.byref(nxt), ctypes.byref(valid), ctypes.byref(normal)))
+    raw = np.zeros(_CPU_STATE_BYTES, dtype=np.uint8)
+    raw[0:8].view("<u8")[0] = seed
+    raw[8:12].view("<i4")[0] = left.value
+    raw[12:16].view("<i4")[0] = 1
+    raw[16:24].view("<u8")[0] = nxt.value
+    raw[24:24 + 8 * 624].view("<u8")[:] = st
+    if valid.value:
+        raw[5024:5032].view("<f8")[0] = normal.value
+        raw[5040:5044].view("<i4")[0] = 1
+    out = torch.from_numpy(raw)
+    with _cpu_state_lock:
+        if len(_cpu_state_cache) >= 16:
+            _cpu_state_cache.pop(next(iter(_cpu_state_cache)))
+        _cpu_state_cache[key] = out
+    return out
+
+
+def rocm_offset(b: "_Batch") -> int:
+    """The Philox offset one seed's torch_rocm draws of b's tensors advance the device
+    generator by (fks_rocm_offset)."""
+    off = ctypes.c_uint64(0)
+    with torch.cuda.device(b.device):
+        N.check(N.load().fks_rocm_offset(ctypes.addressof(b.arr), b.n, ctypes.byref(off)))
+    return int(off.value)
+
+
+def rocm_grid_cap(device=None) -> int:
+    """torch's grid cap for draws on ``device`` (fks_rocm_grid_cap): CUs x (max threads per
+    CU / 256), 2,048 on an MI355X in SPX mode.  The torch_rocm stream of every tensor of more
+    than 256 x cap / 4 elements depends on it (DistributionTemplates.h:50-62), so it is part
+    of the stream's identity on the wire (payload.py)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    cap = ctypes.c_int64(0)
+    with torch.cuda.device(dev):
+        N.check(N.load().fks_rocm_grid_cap(ctypes.byref(cap)))
+    return int(cap.value)
+
+
+def _leave(b: "_Batch", seed) -> None:
+    seed = _seed_u64(seed)
+    torch.manual_seed(seed)  # every generator, as the reference's call does
+    if b.stream_mode == "torch_rocm":
+        idx = b.device.index if b.device.index is not None else torch.cuda.current_device()
+        torch.cuda.default_generators[idx].set_offset(rocm_offset(b))
+    else:
+        torch.set_rng_state(cpu_generator_state(b.arr, b.n, seed))
+
+
+def leave_generators(specs: Sequence[ParamSpec], seed: int, stream_mode=None) -> None:
+    """Leave torch's generators where the reference's torch.manual_seed(seed) and the
+    draws of ``specs`` (every tensor, frozen ones included) leave them."""
+    b = _Batch(specs, stream_mode)
+    if b.device is not None:
+        _leave(b, seed)
+
+
 def directional_step(specs: Sequence[ParamSpec], seeds: Sequence[int], values: Sequence[float],
                      value_is_tensor: bool = False, shard: int = 0, nshards: int = 1, stream_mode=None,
-                     cache_windows: bool = False) -> None:
+                     cache_windows: bool = False, leave_generator: bool = True) -> None:
     """For each (seed, value) in order: p <- p - lr*(value*z + wd*p) over ``specs``.
 
     ``shard``/``nshards``: only the shard-th of nshards equal parts of the parameter stream
     is updated (element sharding across ranks; bit-identical): runs of MT19937 blocks
     (torch_cpu) or of whole Philox rows (torch_rocm).  ``cache_windows``: keep the jumped
     generator windows in the reconstruct window cache (jwin_reserve) so that the next
-    reconstruct of the same list skips the jumps of the seeds it finds there."""
+    reconstruct of the same list skips the jumps of the seeds it finds there.
+    ``leave_generator``: leave torch's generators where the reference's last
+    directional_derivative_step leaves them (see _leave)."""
     if len(seeds) != len(values):
         raise ValueError("seeds and values differ in length")
     if not specs or not len(seeds):
@@ -193,6 +286,8 @@ def directional_step(specs: Sequence[ParamSpec], seeds: Sequence[int], values: S
                                              int(shard), int(nshards), ws.data_ptr(), nbytes,
                                              _stream_handle(b.device)))
         b.finish()
+        if leave_generator:
+            _leave(b, s[-1])
 
 
 # ---------------------------------------------------------------- z-index buffer
@@ -325,7 +420,7 @@ def jwin_stats():
     return int(h.value), int(m.value)
 
 
-def perturb(tensors: Sequence[torch.Tensor], seed: int, scales, stream_mode=None) -> None:
+def perturb(tensors: Sequence[torch.Tensor], seed: int, scales, stream_mode=None, leave_generator: bool = True) -> None:
     """p <- p + scale_i*z for every tensor i (scale = scaling_factor*eps of its group, a
     python double); ``scales`` is one number for all tensors or one per tensor."""
     specs = [ParamSpec(t) for t in tensors]
@@ -347,10 +442,13 @@ def perturb(tensors: Sequence[torch.Tensor], seed: int, scales, stream_mode=None
         N.check(L.fks_perturb(ctypes.addressof(b.arr), b.n, _seed_u64(seed), sc.ctypes.data, ws.data_ptr(), nbytes,
                               _stream_handle(b.device)))
         b.finish()
+        if leave_generator:
+            _leave(b, seed)
 
 
 def perturb_step(specs: Sequence[ParamSpec], seed: int, scales: Sequence[float], value: float,
-                 value_is_tensor: bool = True, update: bool = True, stream_mode=None) -> None:
+                 value_is_tensor: bool = True, update: bool = True, stream_mode=None,
+                 leave_generator: bool = True) -> None:
     """zeroth_order_step's restore perturbation fused with its directional step, in one
     device pass: p <- p + scale_i*z, then (``update``) p <- p - lr*(value*z + wd*p) with
     the same z.  Equal, bit for bit, to ``perturb`` followed by ``directional_step``
@@ -371,10 +469,12 @@ def perturb_step(specs: Sequence[ParamSpec], seed: int, scales: Sequence[float],
                                    N.VALUE_TENSOR if value_is_tensor else N.VALUE_SCALAR, 1 if update else 0,
                                    ws.data_ptr(), nbytes, _stream_handle(b.device)))
         b.finish()
+        if leave_generator:
+            _leave(b, seed)
 
 
 def perturb_step_device(specs: Sequence[ParamSpec], seed: int, scales: Sequence[float], value: torch.Tensor,
-                        apply: torch.Tensor, stream_mode=None) -> None:
+                        apply: torch.Tensor, stream_mode=None, leave_generator: bool = True) -> None:
     """``perturb_step`` with ``value`` (g) and ``apply`` (bool) as device tensors read by the
     kernels when they run: the restore perturbation always, the update iff ``apply`` --
     no host synchronisation on the losses.  g is rounded to each tensor's dtype like a
@@ -397,10 +497,12 @@ def perturb_step_device(specs: Sequence[ParamSpec], seed: int, scales: Sequence[
         N.check(L.fks_perturb_step_dev(ctypes.addressof(b.arr), b.n, _seed_u64(seed), sc.ctypes.data, dv.data_ptr(),
                                        ws.data_ptr(), nbytes, _stream_handle(b.device)))
         b.finish()
+        if leave_generator:
+            _leave(b, seed)
 
 
 def normal_(tensors: Sequence[torch.Tensor], seed: int, frozen: Optional[Sequence[bool]] = None,
-            stream_mode=None) -> None:
+            stream_mode=None, leave_generator: bool = True) -> None:
     """Overwrite every tensor with the z the reference draws for it after manual_seed(seed)."""
     specs = [ParamSpec(t, frozen=bool(frozen[i]) if frozen else False) for i, t in enumerate(tensors)]
     if not specs:
@@ -414,6 +516,8 @@ def normal_(tensors: Sequence[torch.Tensor], seed: int, frozen: Optional[Sequenc
         N.check(L.fks_normal(ctypes.addressof(b.arr), b.n, _seed_u64(seed), ws.data_ptr(), nbytes,
                              _stream_handle(b.device)))
         b.finish()
+        if leave_generator:
+            _leave(b, seed)
 
 
 def _check_delta(b: _Batch, delta: torch.Tensor) -> None:
@@ -427,9 +531,10 @@ def _check_delta(b: _Batch, delta: torch.Tensor) -> None:
 def delta_accumulate(specs: Sequence[ParamSpec], seeds: Sequence[int], coefs: Sequence[float],
                      delta: torch.Tensor, stream_mode=None) -> None:
     """Seed-sharded variant (include/fks.h): delta += f32(coef_s) * z_s for every seed in
-    order, z_s the reference's CPU stream for the spec list (frozen specs draw, are not
-    accumulated); delta is the f32 concatenation of the specs' elements.  The variant
-    draws the torch_cpu stream only: a call that resolves to torch_rocm raises."""
+    order, z_s the reference's stream for the spec list (the call's stream_mode, either
+    stream; frozen specs draw, are not accumulated); delta is the f32 concatenation of the
+    specs' elements.  Draws nothing from torch's generators (the caller leaves them,
+    leave_generators, once the whole list is applied)."""
     if len(seeds) != len(coefs):
         raise ValueError("seeds and coefs differ in length")
     specs = list(specs)
@@ -438,9 +543,6 @@ def delta_accumulate(specs: Sequence[ParamSpec], seeds: Sequence[int], coefs: Se
     b = _Batch(specs, stream_mode)
     if b.device is None:
         return
-    if b.stream_mode != "torch_cpu":
-        raise NotImplementedError("the seed-sharded variant draws the torch_cpu stream only "
-                                  "(stream_mode='torch_cpu' or FKS_STREAM_MODE=torch_cpu)")
     _check_delta(b, delta)
     L = N.load()
     s = np.ascontiguousarray([_seed_u64(x) for x in seeds], dtype=np.uint64)

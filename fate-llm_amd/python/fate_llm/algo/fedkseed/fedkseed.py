@@ -59,9 +59,13 @@ class Trainer:
         self.seed_candidates = seed_candidates
         self.k = len(seed_candidates)
         self.model = None
-        # the federation's z stream: what a WireContext declared, else the first tagged
-        # client history's; every later tagged history must match it
-        self.stream_mode = getattr(ctx, "stream_mode", None) if isinstance(ctx, WireContext) else None
+        # the federation's z stream (and torch_rocm grid cap): what a WireContext declared,
+        # else the first tagged client history's; every later tagged history must match it,
+        # and once known it is declared into the arbiter's own WireContext, so that the
+        # "train_once" records it sends from then on carry it to the clients
+        wire = isinstance(ctx, WireContext)
+        self.stream_mode = ctx.stream_mode if wire else None
+        self.stream_grid = ctx.stream_grid if wire else None
 
     @staticmethod
     def get_clients(ctx) -> list:
@@ -96,20 +100,40 @@ class Trainer:
                 client.put("train_once", (False, payload))
             if sums is None:
                 sums = {s.item(): 0.0 for s in self.seed_candidates}
+            tagged = untagged = 0
             for i, client in enumerate(clients):
                 hist = client.get("direction_derivative_history")
                 stream = getattr(hist, "stream_mode", None)  # payload.History of a tagged record
-                check_stream(self.stream_mode, stream, f"client {i} (guest first, then hosts)")
-                if self.stream_mode is None:
-                    self.stream_mode = stream
+                grid = getattr(hist, "stream_grid", None)
+                check_stream(self.stream_mode, stream, f"client {i} (guest first, then hosts)", self.stream_grid, grid)
+                if stream is None:
+                    untagged += 1
+                else:
+                    tagged += 1
+                    self._adopt_stream(stream, grid)
                 for seed, values in hist.items():
                     seed = int(seed)
                     history.setdefault(seed, []).extend(values)
                     # python float sum of the new values, then one float64 add; a seed
                     # outside the candidates raises KeyError, as in the reference
                     sums[seed] += sum(values)
+            if tagged and untagged:
+                logger.warning(f"FedKSeed arbiter: {untagged} of {tagged + untagged} clients sent untagged histories "
+                               f"(reference parties?) beside clients drawing {self.stream_mode}; their z stream "
+                               "cannot be checked")
             if self.should_stop():
                 break
+
+    def _adopt_stream(self, stream: str, grid) -> None:
+        """Take the first tagged history's stream as the federation's and declare it into
+        the arbiter's WireContext (its later "train_once" records carry it)."""
+        changed = False
+        if self.stream_mode is None:
+            self.stream_mode, changed = stream, True
+        if self.stream_mode == "torch_rocm" and self.stream_grid is None and grid is not None:
+            self.stream_grid, changed = grid, True
+        if changed and isinstance(self.ctx, WireContext):
+            self.ctx.declare_stream_mode(self.stream_mode, self.stream_grid)
 
     def should_stop(self) -> bool:
         return False
@@ -216,15 +240,28 @@ class ClientTrainer:
         torch_rocm on an MI355X, what an unmodified reference client there draws)."""
         return codec.resolve_stream_mode(getattr(self.training_args, "device", None))
 
+    @property
+    def stream_grid(self):
+        """torch_rocm only: the grid cap of the training device (codec.rocm_grid_cap), part of
+        the stream's identity -- torch draws every tensor above 256 x cap / 4 elements in a
+        grid of cap blocks (DistributionTemplates.h:50-62); None for torch_cpu."""
+        if self.stream_mode != "torch_rocm":
+            return None
+        return self._device_grid_cap()
+
+    def _device_grid_cap(self) -> int:
+        return codec.rocm_grid_cap(getattr(self.training_args, "device", None))
+
     def train(self):
-        stream = self.stream_mode
-        logger.info(f"FedKSeed client: z stream {stream} (codec setting {codec.get_stream_mode()!r})")
+        stream, grid = self.stream_mode, self.stream_grid
+        logger.info(f"FedKSeed client: z stream {stream}" + (f", grid cap {grid}" if grid is not None else "") +
+                    f" (codec setting {codec.get_stream_mode()!r})")
         if isinstance(self.ctx, WireContext):
-            self.ctx.declare_stream_mode(stream)  # tags the histories this client sends
+            self.ctx.declare_stream_mode(stream, grid)  # tags the histories this client sends
         for i, sub_ctx in self.ctx.ctxs_range(self.fedkseed_args.num_aggregations):
             logger.info(f"training loop started: {i}")
             should_exit, kwargs = sub_ctx.arbiter.get("train_once")
-            check_stream(stream, kwargs.get("stream_mode"), "the arbiter")
+            check_stream(stream, kwargs.get("stream_mode"), "the arbiter", grid, kwargs.get("stream_grid"))
             if should_exit:
                 break
             history = self.train_once(kwargs["seed_candidates"], kwargs["seed_probabilities"],

@@ -37,11 +37,18 @@ and every other key passes through untouched: opt-in, with no change to the trai
 live (zo_utils.py:47, optimizer.py:170-172: ``device=param.data.device``), so a party on
 a GPU and a party on the CPU apply the same (seed, scalar) list along different
 directions -- silently.  A record can carry the stream its
-sender draws (``stream_mode``: "torch_cpu" or "torch_rocm", two flag bits, no extra
-bytes): the drop-in ``ClientTrainer`` declares its stream into its ``WireContext``, the
-arbiter's ``Trainer`` rejects a history whose stream differs from the others'
-(``StreamMismatchError``), and a client rejects a "train_once" whose declared stream
-differs from its own.  Untagged records (a reference party) decode as before.
+sender draws (``stream_mode``: "torch_cpu" or "torch_rocm", two flag bits) and, for
+torch_rocm, the grid cap of the sender's device (``stream_grid``: CUs x (max threads per CU
+/ 256), a u32 after the header).  torch draws a tensor of n elements in a grid of
+min(ceil(n / 256), cap) blocks and thread idx of it takes elements idx + 256 x grid x (4 j
++ i) (DistributionTemplates.h:50-89), so two GPUs with different caps -- an MI355X in SPX
+mode (2,048) and one in a CPX partition (256), or an MI300X (2,432) -- draw different z for
+every tensor above 256 x cap / 4 elements: the cap is part of the stream.  The drop-in
+``ClientTrainer`` declares its stream into its ``WireContext``, the arbiter's ``Trainer``
+rejects a history whose stream differs from the others' (``StreamMismatchError``) and
+declares the federation's stream into its own records, and a client rejects a
+"train_once" whose declared stream differs from its own.  Untagged records (a reference
+party) decode as before.
 
 Host-side logic only; it touches no parameters and no device.
 """
@@ -69,7 +76,9 @@ _F_SPARSE = 1 << 3        # keys = the candidates: only (index, count) of non-em
 # both kinds: the sender's z stream (bits 8-9, clear of every other flag)
 _F_STREAM_TAGGED = 1 << 8
 _F_STREAM_ROCM = 1 << 9
+_F_STREAM_GRID = 1 << 10  # a u32 grid cap follows the header (torch_rocm only)
 STREAMS = ("torch_cpu", "torch_rocm")
+_GRID = struct.Struct("<I")
 
 _HEADER = struct.Struct("<4sBBHQ")  # magic, version, kind, flags, count
 _U32_MAX = 2 ** 32
@@ -88,14 +97,23 @@ class History(dict):
     original), plus the ``stream_mode`` its sender declared (None if untagged)."""
 
     stream_mode: Optional[str] = None
+    stream_grid: Optional[int] = None
 
 
-def _stream_flags(stream_mode: Optional[str]) -> int:
+def _stream_flags(stream_mode: Optional[str], stream_grid: Optional[int] = None) -> int:
     if stream_mode is None:
+        if stream_grid is not None:
+            raise WireFormatError("a stream_grid needs a stream_mode")
         return 0
     if stream_mode not in STREAMS:
         raise WireFormatError(f"stream_mode must be one of {STREAMS} or None, not {stream_mode!r}")
-    return _F_STREAM_TAGGED | (_F_STREAM_ROCM if stream_mode == "torch_rocm" else 0)
+    if stream_grid is not None:
+        if stream_mode != "torch_rocm":
+            raise WireFormatError("stream_grid belongs to the torch_rocm stream only")
+        if not 0 < int(stream_grid) < 2 ** 32:
+            raise WireFormatError(f"stream_grid must be a positive u32, not {stream_grid!r}")
+    return (_F_STREAM_TAGGED | (_F_STREAM_ROCM if stream_mode == "torch_rocm" else 0)
+            | (_F_STREAM_GRID if stream_grid is not None else 0))
 
 
 def _stream_of(flags: int) -> Optional[str]:
@@ -104,13 +122,37 @@ def _stream_of(flags: int) -> Optional[str]:
     return "torch_rocm" if flags & _F_STREAM_ROCM else "torch_cpu"
 
 
-def check_stream(expected: Optional[str], got: Optional[str], what: str) -> None:
-    """Raise StreamMismatchError when both streams are known and differ."""
-    if expected is not None and got is not None and expected != got:
+def _grid_bytes(stream_grid: Optional[int]) -> bytes:
+    return b"" if stream_grid is None else _GRID.pack(int(stream_grid))
+
+
+def _read_grid(buf: memoryview, flags: int, off: int) -> Tuple[Optional[int], int]:
+    if not flags & _F_STREAM_GRID:
+        return None, off
+    if not flags & _F_STREAM_ROCM:
+        raise WireFormatError("grid cap on a record that is not torch_rocm")
+    (g,), off = _read(buf, off, "<u4", 1)
+    return int(g), off
+
+
+def describe_stream(mode: Optional[str], grid: Optional[int] = None) -> str:
+    return f"{mode} (grid cap {grid})" if mode == "torch_rocm" and grid is not None else str(mode)
+
+
+def check_stream(expected: Optional[str], got: Optional[str], what: str, expected_grid: Optional[int] = None,
+                 got_grid: Optional[int] = None) -> None:
+    """Raise StreamMismatchError when both streams are known and differ: another generator,
+    or torch_rocm on devices of different grid caps (when both caps are known)."""
+    if expected is None or got is None:
+        return
+    if expected != got or (expected == "torch_rocm" and expected_grid is not None and got_grid is not None
+                           and int(expected_grid) != int(got_grid)):
         raise StreamMismatchError(
-            f"{what} draws the {got} z stream, this federation draws {expected}: the parties would apply "
-            "the same (seed, scalar) list along different directions (zo_utils.py:47 draws on the "
-            "parameters' device); set FKS_STREAM_MODE / codec.set_stream_mode alike on every party")
+            f"{what} draws the {describe_stream(got, got_grid)} z stream, this federation draws "
+            f"{describe_stream(expected, expected_grid)}: the parties would apply the same (seed, scalar) list "
+            "along different directions (zo_utils.py:47 draws on the parameters' device, in a grid of at most "
+            "CUs x threads per CU / 256 blocks); set FKS_STREAM_MODE / codec.set_stream_mode alike on every "
+            "party and train every torch_rocm party on devices of one CU count and partition mode")
 
 
 def _keys_array(keys: Sequence[int]) -> Tuple[np.ndarray, bool]:
@@ -140,9 +182,10 @@ def _header(buf, kind: int) -> Tuple[memoryview, int, int]:
     return buf, flags, count
 
 
-def encode_train_once(message: Tuple[bool, Mapping], stream_mode: Optional[str] = None) -> bytes:
+def encode_train_once(message: Tuple[bool, Mapping], stream_mode: Optional[str] = None,
+                      stream_grid: Optional[int] = None) -> bytes:
     """``(should_exit, kwargs)`` of the arbiter's "train_once" put (fedkseed.py:66-68);
-    ``stream_mode``: the federation's z stream, if the arbiter declares one."""
+    ``stream_mode`` / ``stream_grid``: the federation's z stream, if the arbiter declares one."""
     should_exit, kw = message
     seeds = kw["seed_candidates"]
     seeds_np = seeds.detach().cpu().numpy() if torch.is_tensor(seeds) else np.asarray(seeds)
@@ -151,9 +194,10 @@ def encode_train_once(message: Tuple[bool, Mapping], stream_mode: Optional[str] 
     probs = kw.get("seed_probabilities")
     sums: Optional[Mapping[int, float]] = kw.get("direction_derivative_sum")
 
-    flags = (_F_EXIT if should_exit else 0) | (_F_SEEDS_I64 if seeds_i64 else 0) | _stream_flags(stream_mode)
+    flags = ((_F_EXIT if should_exit else 0) | (_F_SEEDS_I64 if seeds_i64 else 0)
+             | _stream_flags(stream_mode, stream_grid))
     kdt = "<i8" if seeds_i64 else "<u4"
-    parts = [seeds_arr.astype(kdt).tobytes()]
+    parts = [_grid_bytes(stream_grid), seeds_arr.astype(kdt).tobytes()]
     if probs is not None:
         p = probs.detach().cpu() if torch.is_tensor(probs) else torch.as_tensor(probs)
         if p.dtype != torch.float32 or p.numel() != k:
@@ -178,9 +222,10 @@ def encode_train_once(message: Tuple[bool, Mapping], stream_mode: Optional[str] 
 def decode_train_once(buf) -> Tuple[bool, Dict]:
     """Inverse of ``encode_train_once``: seeds as ``torch.long``, probabilities as
     ``torch.float32``, sums as a ``dict[int, float]`` in the encoded key order; a tagged
-    record adds ``"stream_mode"`` to the kwargs (the reference reads only its three keys)."""
+    record adds ``"stream_mode"`` (and ``"stream_grid"``) to the kwargs (the reference reads
+    only its three keys)."""
     buf, flags, k = _header(buf, KIND_TRAIN_ONCE)
-    off = _HEADER.size
+    grid, off = _read_grid(buf, flags, _HEADER.size)
     kdt = "<i8" if flags & _F_SEEDS_I64 else "<u4"
     seeds, off = _read(buf, off, kdt, k)
     seed_t = torch.from_numpy(seeds.astype(np.int64))
@@ -203,6 +248,8 @@ def decode_train_once(buf) -> Tuple[bool, Dict]:
     kw = {"seed_candidates": seed_t, "seed_probabilities": probs, "direction_derivative_sum": sums}
     if _stream_of(flags) is not None:
         kw["stream_mode"] = _stream_of(flags)
+        if grid is not None:
+            kw["stream_grid"] = grid
     return bool(flags & _F_EXIT), kw
 
 
@@ -214,12 +261,14 @@ def _values_block(flat: np.ndarray) -> Tuple[int, bytes]:
 
 
 def encode_history(history: Mapping[int, Sequence[float]], candidates: Optional[Sequence[int]] = None,
-                   stream_mode: Optional[str] = None) -> bytes:
+                   stream_mode: Optional[str] = None, stream_grid: Optional[int] = None) -> bytes:
     """A client's ``direction_derivative_history`` (dict seed -> list of g values).
     ``candidates``: the round's seed candidates, known to both ends -- enables the
     sparse form when the history's keys are exactly these seeds in order.
-    ``stream_mode``: the z stream the client drew its steps from (tags the record)."""
-    sflags = _stream_flags(stream_mode)
+    ``stream_mode`` / ``stream_grid``: the z stream the client drew its steps from (tags the
+    record)."""
+    sflags = _stream_flags(stream_mode, stream_grid)
+    gbytes = _grid_bytes(stream_grid)
     keys = [int(s) for s in history.keys()]
     counts = np.fromiter((len(v) for v in history.values()), dtype="<u4", count=len(keys))
     flat = np.fromiter((float(x) for v in history.values() for x in v), dtype="<f8",
@@ -227,19 +276,19 @@ def encode_history(history: Mapping[int, Sequence[float]], candidates: Optional[
     vflag, vbytes = _values_block(flat)
     if candidates is not None and keys == [int(c) for c in candidates]:
         nz = np.nonzero(counts)[0]
-        return (_HEADER.pack(MAGIC, VERSION, KIND_HISTORY, _F_SPARSE | vflag | sflags, len(nz))
+        return (_HEADER.pack(MAGIC, VERSION, KIND_HISTORY, _F_SPARSE | vflag | sflags, len(nz)) + gbytes
                 + nz.astype("<u4").tobytes() + counts[nz].tobytes() + vbytes)
     karr, ki64 = _keys_array(keys)
     flags = (_F_KEYS_I64 if ki64 else 0) | vflag | sflags
-    return (_HEADER.pack(MAGIC, VERSION, KIND_HISTORY, flags, len(keys))
+    return (_HEADER.pack(MAGIC, VERSION, KIND_HISTORY, flags, len(keys)) + gbytes
             + karr.astype("<i8" if ki64 else "<u4").tobytes() + counts.tobytes() + vbytes)
 
 
 def decode_history(buf, candidates: Optional[Sequence[int]] = None) -> Dict[int, List[float]]:
     """Inverse of ``encode_history``; a tagged record decodes to a ``History`` carrying
-    the sender's ``stream_mode``."""
+    the sender's ``stream_mode`` and ``stream_grid``."""
     buf, flags, n = _header(buf, KIND_HISTORY)
-    off = _HEADER.size
+    grid, off = _read_grid(buf, flags, _HEADER.size)
     if flags & _F_SPARSE:
         if candidates is None:
             raise WireFormatError("sparse history record needs the round's seed candidates")
@@ -256,6 +305,7 @@ def decode_history(buf, candidates: Optional[Sequence[int]] = None) -> Dict[int,
     out: Dict[int, List[float]] = {} if stream is None else History()
     if stream is not None:
         out.stream_mode = stream
+        out.stream_grid = grid
     pos = 0
     if flags & _F_SPARSE:
         cand = [int(c) for c in candidates]
@@ -283,12 +333,12 @@ class _WireParty:
         self._party, self._state, self._role = party, state, role
 
     def put(self, key, value):
-        stream = self._state.get(_STREAM_KEY)
+        stream, grid = self._state.get(_STREAM_KEY), self._state.get(_GRID_KEY)
         if key == "train_once":
             self._state[self._role] = [int(s) for s in value[1]["seed_candidates"]]
-            value = encode_train_once(value, stream)
+            value = encode_train_once(value, stream, grid)
         elif key == "direction_derivative_history":
-            value = encode_history(value, self._state.get(self._role), stream)
+            value = encode_history(value, self._state.get(self._role), stream, grid)
         return self._party.put(key, value)
 
     def get(self, key):
@@ -298,7 +348,8 @@ class _WireParty:
         if key == "train_once":
             value = decode_train_once(value)
             self._state[self._role] = value[1]["seed_candidates"].tolist()
-            check_stream(self._state.get(_STREAM_KEY), value[1].get("stream_mode"), "the arbiter")
+            check_stream(self._state.get(_STREAM_KEY), value[1].get("stream_mode"), "the arbiter",
+                         self._state.get(_GRID_KEY), value[1].get("stream_grid"))
         elif key == "direction_derivative_history":
             value = decode_history(value, self._state.get(self._role))
         return value
@@ -308,29 +359,37 @@ class _WireParty:
 
 
 _STREAM_KEY = object()  # WireContext state: the z stream this party declared
+_GRID_KEY = object()    # ... and its torch_rocm grid cap
 
 
 class WireContext:
     """Wraps a federation context: ``ctxs_range`` yields wrapped sub-contexts whose
     ``guest``, ``hosts`` and ``arbiter`` parties move the FedKSeed round payloads in
     the compact format.  Both ends of a link must be wrapped.  ``stream_mode``: the z
-    stream this party draws ("torch_cpu" / "torch_rocm"), carried by every record it
-    sends; the drop-in ClientTrainer declares its own (``declare_stream_mode``)."""
+    stream this party draws ("torch_cpu" / "torch_rocm"), and ``stream_grid`` its torch_rocm
+    grid cap, carried by every record it sends; the drop-in ClientTrainer declares its own
+    (``declare_stream_mode``)."""
 
-    def __init__(self, ctx, _state=None, stream_mode: Optional[str] = None):
+    def __init__(self, ctx, _state=None, stream_mode: Optional[str] = None, stream_grid: Optional[int] = None):
         self._ctx = ctx
         self._state = {} if _state is None else _state  # role -> seed candidates of the link
         if stream_mode is not None:
-            self.declare_stream_mode(stream_mode)
+            self.declare_stream_mode(stream_mode, stream_grid)
 
-    def declare_stream_mode(self, stream_mode: Optional[str]) -> None:
-        _stream_flags(stream_mode)  # validates
-        check_stream(self._state.get(_STREAM_KEY), stream_mode, "this party")
+    def declare_stream_mode(self, stream_mode: Optional[str], stream_grid: Optional[int] = None) -> None:
+        _stream_flags(stream_mode, stream_grid)  # validates
+        check_stream(self._state.get(_STREAM_KEY), stream_mode, "this party", self._state.get(_GRID_KEY), stream_grid)
         self._state[_STREAM_KEY] = stream_mode
+        if stream_grid is not None or stream_mode != "torch_rocm":
+            self._state[_GRID_KEY] = stream_grid
 
     @property
     def stream_mode(self) -> Optional[str]:
         return self._state.get(_STREAM_KEY)
+
+    @property
+    def stream_grid(self) -> Optional[int]:
+        return self._state.get(_GRID_KEY)
 
     def ctxs_range(self, n):
         for i, sub in self._ctx.ctxs_range(n):

@@ -63,7 +63,9 @@ def directional_derivative_step(
 
     lr / weight_decay default to the first group's values and then stick for every
     later group, exactly as the reference resolves them.  Parameters are updated in
-    place on the GPU; ``torch.manual_seed`` is still called for its global side effect.
+    place on the GPU, and torch's generators are left where the reference's
+    torch.manual_seed and draws leave them (the generator of the parameters' device past
+    this seed's z).
     """
     torch.manual_seed(directional_derivative_seed)
     specs = codec.resolve_groups(param_groups, lr=lr, weight_decay=weight_decay)
@@ -83,10 +85,10 @@ def reconstruct_(param_groups: List[dict], seeds: Sequence[int], values: Sequenc
         return 0
     specs = codec.resolve_groups(param_groups, lr=lr, weight_decay=weight_decay)
     # the same list comes back every round (the arbiter's fixed seed candidates): keep the
-    # jumped generator windows for the next reconstruct (codec.jwin_reserve, a speed cache)
+    # jumped generator windows for the next reconstruct (codec.jwin_reserve, a speed cache).
+    # torch's generators end where the last applied seed's draws leave them (codec._leave).
     codec.directional_step(specs, [s for s, _ in keep], [g for _, g in keep], value_is_tensor=False,
                            cache_windows=True)
-    torch.manual_seed(keep[-1][0])  # the global generator was last seeded with the last applied seed
     return len(keep)
 
 
@@ -149,7 +151,7 @@ def reconstruct_seed_sharded_(param_groups: List[dict], seeds: Sequence[int], va
     if distributed:  # also at world size 1: the group's collective library sums (an identity)
         dist.all_reduce(delta, op=dist.ReduceOp.SUM, group=process_group)
     codec.delta_apply(specs, delta, [decay] * len(specs))
-    torch.manual_seed(keep[-1][0])
+    codec.leave_generators(specs, keep[-1][0])  # where the reference's last seed leaves them
     return len(keep)
 
 

@@ -16,10 +16,13 @@
  *                            zo_utils.py:47 / optimizer.py:170-172, for one seed, written
  *                            into the tensors (stream parity checks)
  *
- * Numerics: the z stream is the one torch's CPU generator produces after
- * torch.manual_seed(seed) (mt19937 + normal_fill Box-Muller, fp32 via the AVX2
- * Cephes kernel, bf16/f16 per-op rounded), i.e. the reference run with CPU
- * tensors, and every update op is rounded exactly as the reference's torch ops.
+ * Numerics: the z stream is the one the reference draws after torch.manual_seed(seed)
+ * where its parameters live (zo_utils.py:47 draws on param.data.device), selected per
+ * call by FKS_STREAM_ROCM: torch's HIP-device generator (Philox4x32-10 + rocrand
+ * Box-Muller; the Python drop-in's default for tensors on a GPU, codec.py "auto") or
+ * torch's CPU generator (mt19937 + normal_fill Box-Muller, fp32 via the AVX2 Cephes
+ * kernel, bf16/f16 per-op rounded; a reference client training on the CPU).  Every
+ * update op is rounded exactly as the reference's torch ops.
  *
  * Conventions (all entry points):
  *  - plain pointers and sizes only; tensor data are DEVICE pointers, contiguous,
@@ -142,6 +145,31 @@ int fks_shard_census(const fks_tensor* t, int32_t nt, int32_t shard, int32_t nsh
 /* Number of 32-bit generator words the tensor list consumes per seed (its stream length). */
 int fks_stream_length(const fks_tensor* t, int32_t nt, int64_t* words);
 
+/* ---- where the reference leaves torch's global generators ----
+ * The reference calls torch.manual_seed(seed) and then draws (zo_utils.py:42,47;
+ * optimizer.py:165,170-172), so after a call the generator of the tensors' device has
+ * advanced past the seed's draws; every later draw from it (a sampler's permutation, the
+ * model's dropout in the zeroth-order closure) starts there.  The codec draws nothing
+ * from torch's generators; these give the caller the state to leave behind.
+ *
+ * fks_cpu_generator_end (host only, no device needed): torch's CPU generator after
+ * torch.manual_seed(seed) and the CPU-stream draws of the tensor list -- at::mt19937's
+ * state_ (624 untempered words), left_ and next_ (MT19937RNGEngine.h:115-175), and
+ * CPUGeneratorImpl's cached normal_distribution<double> value (valid iff numel < 16
+ * tensors left the second value of a Box-Muller pair, DistributionsHelper.h:189-221).
+ *
+ * fks_rocm_offset: the Philox offset torch's generator of the CURRENT device advances by
+ * for one seed's FKS_STREAM_ROCM draws of the list (DistributionTemplates.h:50-62,
+ * :111-133, including the extra reservations of tensors past 2^31 bytes).
+ * fks_rocm_grid_cap: the current device's grid cap of torch's draws, CUs x
+ * (maxThreadsPerCU / 256) (2,048 on an MI355X in SPX mode); the FKS_STREAM_ROCM stream of a
+ * tensor of more than 256 x cap / 4 elements depends on it, so parties of one federation
+ * must agree on it (payload.py carries it). */
+int fks_cpu_generator_end(const fks_tensor* t, int32_t nt, uint64_t seed, uint32_t* state624, int32_t* left,
+                          uint32_t* next, int32_t* normal_valid, double* normal);
+int fks_rocm_offset(const fks_tensor* t, int32_t nt, uint64_t* offset);
+int fks_rocm_grid_cap(int64_t* blocks);
+
 /* Instrumentation (bench.py): while enabled, every kernel launch is bracketed by HIP
  * events on the caller's stream; fks_profile_end synchronises them and returns the
  * summed device time of the apply and jump kernels and their launch counts. */
@@ -220,7 +248,8 @@ int fks_perturb_step_dev(const fks_tensor* t, int32_t nt, uint64_t seed, const d
  * element e: delta[cum_i + e] = fmaf(f32(coefs[s]), z_s(i, e), delta[cum_i + e]),
  * cum_i = sum of numel over tensors before i (the delta buffer is the tensors'
  * concatenation, f32, 8-byte aligned, device memory); z_s is the reference's stream
- * for seeds[s] and the tensor's dtype.  lr/wd/flags of the tensors are ignored (the
+ * for seeds[s] and the tensor's dtype (either stream: FKS_STREAM_ROCM selects torch's
+ * device generator, the counter-mode stream that needs no jumps).  lr/wd/flags of the tensors are ignored (the
  * caller folds them into coefs).  Workspace: fks_delta_workspace_size.
  * fks_delta_apply: for every non-frozen tensor i: p = dtype(fmaf(f32(decay[i]), p,
  * -delta[cum_i + e])).                                                               */

@@ -16,6 +16,21 @@ for p in (ROOT, PKG_PY):
 # (test_stream_tag.py, test_gpu_torch_rocm.py).  Subprocesses inherit this.
 os.environ.setdefault("FKS_STREAM_MODE", "torch_cpu")
 
+# A tree that arrives without libfks.so / liboracle.so is built here, in a subprocess, before
+# any test touches the GPU (__graft_entry__.ensure_built: make -C fate-llm_amd, make -C oracle).
+import __graft_entry__  # noqa: E402
+
+_COMPILED = __graft_entry__.ensure_built()
+
+
+def pytest_report_header(config):
+    from fate_llm.algo.fedkseed import _native
+    try:
+        bid = _native.build_id()
+    except OSError as e:  # reported, and every codec test then fails loudly
+        bid = f"not loadable ({e})"
+    return f"libfks.so build id {bid}; compile commands run by this session's conftest: {_COMPILED}"
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP) device; parity tests of the product path")

@@ -137,3 +137,43 @@ def test_invalid_inputs_rejected():
     arr[0].data = 16
     arr[0].dtype = 7
     assert L.fks_workspace_size(ctypes.addressof(arr), 1, 1, ctypes.byref(nbytes)) < 0
+
+
+_TORCH_DT = {0: "float32", 1: "bfloat16", 2: "float16"}
+
+
+@pytest.mark.parametrize("layout", [
+    [(3, 0), (20, 0)],                         # serial pair cached, then a tail recompute
+    [(5, 1), (7, 2), (1000, 1), (1, 0)],       # caches consumed and refilled across tensors
+    [(4096, 0), (5, 0)],
+    [(16, 1)],                                 # no serial draw: no cached value
+    [(100000, 0), (3, 1), (17, 2)],
+    [(0, 0)],                                  # draws nothing: the freshly seeded state
+    [(624 * 3, 1)],                            # ends exactly on a block boundary
+    [(3 * 10**7 + 5, 0), (2, 1)],              # many blocks (a jump far into the stream)
+])
+@pytest.mark.parametrize("seed", [0, 12345, 2**40 + 7])
+def test_cpu_generator_end_matches_torch(layout, seed):
+    """fks_cpu_generator_end, assembled into torch's CPU generator state by
+    codec.cpu_generator_state, equals torch's own CPU generator after torch.manual_seed(seed)
+    and torch.normal draws of the same sizes and dtypes (zo_utils.py:42,47 on CPU tensors):
+    byte for byte, and the next draws agree."""
+    import torch
+
+    from fate_llm.algo.fedkseed import codec
+    N, _ = _lib()
+    arr = (N.FksTensor * len(layout))()
+    for i, (n, d) in enumerate(layout):
+        arr[i].data = 16 if n else None  # never dereferenced
+        arr[i].numel = n
+        arr[i].dtype = d
+    ours = codec.cpu_generator_state(arr, len(layout), seed)
+    torch.manual_seed(seed)
+    for n, d in layout:
+        torch.normal(mean=0, std=1, size=(n,), dtype=getattr(torch, _TORCH_DT[d]))
+    ref = torch.get_rng_state()
+    assert torch.equal(ours, ref)
+    follow = torch.randn(7, dtype=torch.float64), torch.randint(0, 2**31, (5,)), torch.normal(0, 1, (3,))
+    torch.set_rng_state(ours)
+    again = torch.randn(7, dtype=torch.float64), torch.randint(0, 2**31, (5,)), torch.normal(0, 1, (3,))
+    assert all(torch.equal(a, b) for a, b in zip(follow, again))
