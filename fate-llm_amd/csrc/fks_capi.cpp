@@ -992,22 +992,17 @@ void phx_geometry(const fks_tensor* t, int nt, const double* scales, PhxPlan* P,
     const bool live = !(t[i].flags & FKS_FROZEN);
     const uint64_t base = delta_base ? delta_base + 4 * (uint64_t)(elems - n) : (uint64_t)(uintptr_t)t[i].data;
     const size_t ses = delta_base ? 4 : es;  // bytes per stored element
-    // distribution_nullary_kernel (DistributionTemplates.h:111-133): the draw of m elements
-    // first reserves its own offset increment, then -- when the iterator cannot use 32-bit
-    // indexing -- draws the two halves TensorIterator::with_32bit_indexing splits it into
-    // (first floor(m / 2) elements, then the rest, recursively), each reserving its own.
-    // A piece is a table entry of its own (its elements, stride and offset).
-    auto draw = [&](auto&& self, int64_t start, int64_t m) -> void {
+    // distribution_nullary_kernel (DistributionTemplates.h:111-133) first reserves the
+    // offset increment of the whole tensor; when the iterator cannot use 32-bit indexing it
+    // then draws each piece TensorIterator::with_32bit_indexing yields -- halves split until
+    // they fit, first floor(m / 2) elements then the rest, in order -- as a call of its own,
+    // which reserves that piece's increment.  A piece is a table entry of its own (its
+    // elements, stride and offset).
+    auto emit = [&](int64_t start, int64_t m) {
       int64_t stride = 0, J = 0;
       phx_policy(m, max_grid, stride, J);
       const uint64_t my_off4 = off4;
       off4 += (uint64_t)J;
-      if (!phx_fits32(m, es)) {
-        const int64_t h = m / 2;
-        self(self, start, h);
-        self(self, start + h, m - h);
-        return;
-      }
       if (!live) return;
       PhxTensor x{};
       x.ptr = base + (uint64_t)start * ses;
@@ -1018,14 +1013,31 @@ void phx_geometry(const fks_tensor* t, int nt, const double* scales, PhxPlan* P,
       x.dtype = t[i].dtype;
       x.lr = t[i].lr;
       x.wd = t[i].wd;
-      x.flags = (t[i].flags & FKS_HAS_WD) | ((x.ptr % 16u) == 0 ? kPhxP16 : 0u);
+      x.flags = (t[i].flags & FKS_HAS_WD) | ((x.ptr % 16u) == 0 ? kPhxP16 : 0u) |
+                (((uint64_t)start * es) % 16u == 0 ? kPhxFresh16 : 0u);
       x.ps = scales ? (float)scales[i] : 0.0f;
       tab.push_back(x);
       elem0.push_back(elems - n + start);
       tensor_of.push_back(i);
       items += stride * J;
     };
-    draw(draw, 0, n);
+    auto pieces = [&](auto&& self, int64_t start, int64_t m) -> void {
+      if (phx_fits32(m, es)) {
+        emit(start, m);
+        return;
+      }
+      const int64_t h = m / 2;
+      self(self, start, h);
+      self(self, start + h, m - h);
+    };
+    if (phx_fits32(n, es)) {
+      emit(0, n);
+    } else {
+      int64_t stride = 0, J = 0;
+      phx_policy(n, max_grid, stride, J);
+      off4 += (uint64_t)J;  // the whole tensor's reservation, before the pieces' own
+      pieces(pieces, 0, n);
+    }
   }
   P->off4_total = off4;
   P->tensor_of = std::move(tensor_of);
@@ -1076,9 +1088,10 @@ PhxPlan* get_phx_plan(const fks_tensor* t, int nt, const double* scales, uint64_
   P->last_use = ++g_cache_clock;
   (void)hipGetDevice(&P->device);
   const size_t bytes = std::max<size_t>(sizeof(PhxTensor) * P->tab.size(), 256);
-  if (hipMalloc(&P->dev, bytes) != hipSuccess) {
+  if (const hipError_t e = hipMalloc(&P->dev, bytes); e != hipSuccess) {
     delete P;
-    throw Error(-FKS_ENOMEM, "torch_rocm plan hipMalloc");
+    throw Error(-FKS_ENOMEM, std::string("torch_rocm plan hipMalloc: ") + hipGetErrorString(e) + " (" +
+                                 std::to_string(bytes) + " bytes)");
   }
   if (!P->tab.empty() &&
       hipMemcpy(P->dev, P->tab.data(), sizeof(PhxTensor) * P->tab.size(), hipMemcpyHostToDevice) != hipSuccess) {

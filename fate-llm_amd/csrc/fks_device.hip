@@ -2695,12 +2695,15 @@ __device__ __forceinline__ void phx_seeds(const PhiloxArgs& a, const PhxTensor& 
   const float gd = dv ? dev_value_g<DT>(a.gdev) : 0.0f;
   const PhxRound1 r1 = philox_round1(T.off4 + j, idx);
   f32x2_t pA = {p[0], p[1]}, pB = {p[2], p[3]};
-  // f16: which elements torch's unrolled path (one rounding) takes (mul_f16_ref)
+  // f16: which elements torch's unrolled path (one rounding) takes (mul_f16_ref): the
+  // partial last block of the launch, or every element of a launch whose fresh tensors do
+  // not start 16-byte aligned (a later 32-bit piece of a tensor past 2^31 bytes)
   bool tail[4] = {false, false, false, false};
   const bool p16 = (T.flags & kPhxP16) != 0;
   if (DT == FKS_F16) {
+    const bool fresh16 = (T.flags & kPhxFresh16) != 0;
 #pragma unroll
-    for (int i = 0; i < 4; i++) tail[i] = e[i] >= T.numel - T.numel % kTorchHalfBlockWork;
+    for (int i = 0; i < 4; i++) tail[i] = !fresh16 || e[i] >= T.numel - T.numel % kTorchHalfBlockWork;
   }
   for (int k = 0; k < a.nseeds; k++) {
     const uint64_t seed = a.seeds[k];  // wave-uniform: scalar loads

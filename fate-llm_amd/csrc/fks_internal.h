@@ -230,6 +230,10 @@ static_assert(sizeof(PhxTensor) == 56, "PhxTensor layout");
 // PhxTensor::flags: the parameter's data is 16-byte aligned (an f16 tensor then takes torch's
 // 8-wide vectorized elementwise path; fks_device.hip mul_f16_ref)
 constexpr uint32_t kPhxP16 = 1u << 8;
+// ... and the entry's first element sits 16-byte aligned in a freshly allocated tensor of the
+// parameter's size (z, g z, the update's temporaries): false only for the later pieces of a
+// tensor past 2^31 bytes, whose 32-bit-indexed launches start mid-tensor
+constexpr uint32_t kPhxFresh16 = 1u << 9;
 // torch's elementwise kernels on ROCm (ATen/native/cuda/CUDALoops.cuh): a 2-byte tensor is
 // processed in blocks of 256 threads x 8 elements; a partial last block takes the unrolled path
 constexpr int64_t kTorchHalfBlockWork = 2048;

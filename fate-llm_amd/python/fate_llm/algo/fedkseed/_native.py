@@ -64,6 +64,10 @@ def load():
             return _lib
         if not os.path.exists(LIB_PATH):
             raise OSError(f"{LIB_PATH} not built; run `make -C fate-llm_amd` (hipcc, gfx950)")
+        # torch's HIP runtime first: loading libfks.so (linked against /opt/rocm's) into a
+        # process that has not imported torch yet leaves the library with a HIP runtime that
+        # sees no device once torch brings in its own ("no ROCm-capable device is detected")
+        import torch  # noqa: F401
         L = ctypes.CDLL(LIB_PATH)
         P, c_i32, c_u64, c_sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64, ctypes.c_size_t
         L.fks_workspace_size.argtypes = [P, c_i32, c_i32, ctypes.POINTER(c_sz)]

@@ -24,6 +24,7 @@ _COMPILED = __graft_entry__.ensure_built()
 
 
 def pytest_report_header(config):
+    import torch  # noqa: F401  (before libfks.so: _native.load)
     from fate_llm.algo.fedkseed import _native
     try:
         bid = _native.build_id()

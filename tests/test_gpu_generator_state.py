@@ -177,3 +177,22 @@ def test_seed_sharded_reconstruct_leaves_the_generators():
     finally:
         codec.set_stream_mode("torch_cpu")
     _assert_states(_states(dev), want, "seed-sharded reconstruct")
+
+
+def test_grid_cap_is_torchs():
+    """The grid cap the library draws with (fks_capi.cpp phx_geometry) and carries on the
+    wire is the one torch's calc_execution_policy derives (DistributionTemplates.h:55-57)
+    from the device properties; and a tensor of exactly 256 x cap x 4 + 1 elements -- one
+    past a single loop iteration of the full grid -- draws torch's values."""
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    props = torch.cuda.get_device_properties(dev)
+    cap = props.multi_processor_count * (props.max_threads_per_multi_processor // 256)
+    assert codec.rocm_grid_cap(dev) == cap
+    n = 256 * cap * 4 + 1
+    torch.manual_seed(77)
+    want = torch.normal(mean=0, std=1, size=(n,), device=dev)
+    got = torch.empty(n, device=dev)
+    codec.normal_([got], 77, stream_mode="torch_rocm")
+    torch.cuda.synchronize()
+    assert torch.equal(got.view(torch.int32), want.view(torch.int32))

@@ -3,9 +3,10 @@
 **Past 2^31 bytes.** torch's distribution_nullary_kernel (ATen/native/cuda/
 DistributionTemplates.h:111-133) first reserves the whole tensor's Philox offset
 increment, then -- when the iterator cannot use 32-bit indexing (largest byte offset past
-INT32_MAX) -- draws the halves TensorIterator::with_32bit_indexing splits it into, first
-floor(n / 2) elements then the rest, recursively, each half with its own launch geometry
-and its own reservation.  fks_capi.cpp phx_geometry restates that: each piece is a table
+INT32_MAX) -- draws each piece TensorIterator::with_32bit_indexing yields (halves split until
+they fit: first floor(n / 2) elements then the rest, recursively) as a call of its own, with
+its own launch geometry and its own reservation; the intermediate halves reserve nothing
+(the 4.4 GB case, four pieces, pins that).  fks_capi.cpp phx_geometry restates that: each piece is a table
 entry of its own.  Oracle: torch.normal(device="cuda") itself, and the reference's update
 expression as torch ops on the device (oracle/torch_replica.py).  Bar: bit-exact, and the
 device generator's offset after the call equal to torch's.
