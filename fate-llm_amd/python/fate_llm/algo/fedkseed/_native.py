@@ -29,7 +29,7 @@ EXPORTED = (
     "fks_shard_census", "fks_perturb_step", "fks_delta_workspace_size", "fks_delta_accumulate", "fks_delta_apply",
     "fks_plan_cache_clear", "fks_perturb_step_dev", "fks_device_selfcheck", "fks_build_id",
     "fks_zindex_size", "fks_zindex_attach", "fks_jwin_size", "fks_jwin_size_shard", "fks_jwin_attach",
-    "fks_jwin_stats", "fks_cpu_generator_end", "fks_rocm_offset", "fks_rocm_grid_cap",
+    "fks_jwin_stats", "fks_cpu_generator_end", "fks_rocm_offset", "fks_rocm_grid_cap", "fks_source_id",
 )
 
 
@@ -78,6 +78,7 @@ def load():
         L.fks_abi_version.restype = c_i32
         L.fks_build_target.restype = ctypes.c_char_p
         L.fks_build_id.restype = ctypes.c_char_p
+        L.fks_source_id.restype = ctypes.c_char_p
         L.fks_host_jump_window.argtypes = [c_u64, ctypes.c_int64, P]
         L.fks_host_tables.argtypes = [c_i32, P, P, P, c_i32]
         L.fks_directional_step_shard.argtypes = [P, c_i32, P, P, c_i32, c_i32, c_i32, c_i32, P, c_sz, P]
@@ -120,6 +121,11 @@ def load():
 def build_id() -> str:
     """16 hex digits identifying the device code of the loaded libfks.so (fks_build_id)."""
     return load().fks_build_id().decode()
+
+
+def source_id() -> str:
+    """16 hex digits identifying the sources the loaded libfks.so was built from (fks_source_id)."""
+    return load().fks_source_id().decode()
 
 
 def check(rc: int) -> None:

@@ -259,12 +259,23 @@ def run_client(rank, args, arbiter_rank):
                 for _ in range(args.steps):
                     opt.kseed_zeroth_order_step(closure)
                 hist = opt.directional_derivative_history
+                if args.d2h:
+                    # the path ends in host memory (the north star's H<->D clause): the trained
+                    # parameters back into pinned host buffers, timed on their own
+                    torch.cuda.synchronize()
+                    td = time.perf_counter()
+                    if not hasattr(self, "_host"):  # one pinned buffer per parameter, kept across rounds
+                        self._host = [torch.empty(p.shape, dtype=p.dtype, pin_memory=True) for p in model.parameters()]
+                    for buf, p in zip(self._host, model.parameters()):
+                        buf.copy_(p.detach(), non_blocking=True)
+                    torch.cuda.synchronize()
+                    self._t["d2h_s"] = time.perf_counter() - td
                 del model, opt
             torch.cuda.synchronize()
             end = time.perf_counter()
             rec = dict(self._t)
             t0 = rec.pop("t0")
-            rec["local_steps_s"] = end - t0 - rec["materialize_s"] - rec["reconstruct_s"]
+            rec["local_steps_s"] = end - t0 - rec["materialize_s"] - rec["reconstruct_s"] - rec.get("d2h_s", 0.0)
             rec["client_round_s"] = end - t0
             rec["round"] = len(timings)
             timings.append(rec)
@@ -368,6 +379,8 @@ def main(argv=None):
                     help="ClientTrainer model_0_placement")
     ap.add_argument("--driver", choices=("optimizer", "trainer"), default="optimizer")
     ap.add_argument("--wire", action="store_true", help="round payloads in the compact binary format")
+    ap.add_argument("--d2h", action="store_true",
+                    help="optimizer driver: copy the trained parameters back to pinned host memory, timed (d2h_s)")
     ap.add_argument("--record", action="store_true", help="return every client's round for an oracle replay")
     ap.add_argument("--record-prefix", type=int, default=PREFIX,
                     help="parameters of the first tensor --record reports (0: the whole tensor)")

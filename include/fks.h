@@ -273,6 +273,11 @@ const char* fks_build_target(void);
  * build (profiles/pmc_*.json) carry it, so a report can check that they belong to the
  * kernels it times (bench.py). */
 const char* fks_build_id(void);
+/* Identity of the sources: 16 hex digits of the SHA-256 of the concatenated source files the
+ * library was built from (fate-llm_amd/Makefile SRCS), so that a prebuilt libfks.so can be
+ * checked against the tree it travels with (__graft_entry__.ensure_built rebuilds on a
+ * mismatch). */
+const char* fks_source_id(void);
 
 /* Host-only self checks (no device needed): the jump-ahead window of `seed` at
  * stream block `block` (= the 624-word generator state before block `block` is

@@ -30,7 +30,12 @@ def pytest_report_header(config):
         bid = _native.build_id()
     except OSError as e:  # reported, and every codec test then fails loudly
         bid = f"not loadable ({e})"
-    return f"libfks.so build id {bid}; compile commands run by this session's conftest: {_COMPILED}"
+    try:
+        sid = _native.source_id()
+    except OSError:
+        sid = None
+    return (f"libfks.so build id {bid}, source id {sid} (this tree: {__graft_entry__.source_id()}); "
+            f"compile commands run by this session's conftest: {_COMPILED}")
 
 
 def pytest_configure(config):

@@ -37,6 +37,9 @@ def test_header_symbols_exported():
     assert L.fks_abi_version() == N.ABI_VERSION
     assert L.fks_build_target() == b"gfx950"
     assert re.fullmatch(r"[0-9a-f]{16}", N.build_id())
+    # the library in the tree was built from the sources beside it (__graft_entry__.ensure_built)
+    import __graft_entry__
+    assert N.source_id() == __graft_entry__.source_id()
 
 
 def test_fks_tensor_layout_matches_header():

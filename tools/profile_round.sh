@@ -26,5 +26,6 @@ timeout -k 10 400 python3 -u bench.py > gpurun_out/${TAG}_bench_default.log 2>&1
 tail -1 gpurun_out/${TAG}_bench_default.log
 rm -rf gpurun_out/${TAG}_trace
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace -o run --output-format csv -- \
-  python3 -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --alt-wd 0.0 > gpurun_out/${TAG}_bench_trace_run.log 2>&1 || exit 93
+  python3 -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --alt-wd 0.0 --alt-stream-steps 1 --no-hd \
+  > gpurun_out/${TAG}_bench_trace_run.log 2>&1 || exit 93
 tail -1 gpurun_out/${TAG}_bench_trace_run.log
