@@ -70,9 +70,9 @@ VALU_MIX_CYCLES = 4.43
 VALU_MIX_CEILING_TLANEOPS = 1024 * 64 * 2.4e9 / VALU_MIX_CYCLES / 1e12
 # per-launch counters of the bf16 slice kernel (fks_apply_bs_kernel), tools/summarize_pmc2.py: the
 # weight-decay chain (wd != 0) and the zero-weight-decay chain (kModeUpdateWd0)
-PMC_SUMMARIES = {"wd": "pmc_apply_r05w_full.json", "wd0": "pmc_apply_r05w_wd0.json"}
+PMC_SUMMARIES = {"wd": "pmc_apply_r06_full.json", "wd0": "pmc_apply_r06_wd0.json"}
 # the torch_rocm stream's kernel (fks_philox_vec_kernel, 32-seed launches) at wd 0.0
-PMC_SUMMARY_PHX = "pmc_apply_r05w_phx_wd0.json"
+PMC_SUMMARY_PHX = "pmc_apply_r06_phx_wd0.json"
 
 
 def llama7b_shapes():

@@ -28,3 +28,4 @@ run log=identity 's = s.replace("const float radius = radius_sqrt(-2.0f * cephes
 run sincos=identity 's = s.replace("  cephes_sincosf_nonneg(6.28318548202514648438f * d2, s, c);\n  z1", "  s = d2; c = 6.28318548202514648438f * d2;\n  z1")'
 run temper=identity 's = s.replace("  const u32x2_t t = temper_pair_u24(w);\n  const float d1", "  const u32x2_t t = w;\n  const float d1")'
 run z=raw_words 's = s.replace("  const u32x2_t t = temper_pair_u24(w);\n  const float d1 = (float)t.x * (1.0f / 16777216.0f);\n  const float d2 = (float)t.y * (1.0f / 16777216.0f);\n  const float radius = radius_sqrt(-2.0f * cephes_logf(1.0f - d1));\n  float s, c;\n  cephes_sincosf_nonneg(6.28318548202514648438f * d2, s, c);\n  z1 = __fmaf_rn(radius, c, 0.0f);\n  z2 = __fmaf_rn(radius, s, 0.0f);", "  z1 = __uint_as_float(r1); z2 = __uint_as_float(r2);")'
+run twist=none 's = s.replace("      twist_all(plan, nseeds);  // the raw words of stream block b", "      (void)plan;")'
