@@ -389,7 +389,8 @@ def run(args, world, rank, local):
     # the headline draws torch's CPU-generator stream (the oracle-pinned one: a reference
     # client training on the CPU, the tutorial's configuration); the drop-in's default
     # "auto" would draw the torch_rocm stream on a GPU, which alt_stream times beside it
-    codec.set_stream_mode("torch_cpu")
+    codec.set_stream_mode(args.stream)
+    rocm = args.stream == "torch_rocm"
     dtype = torch.bfloat16
     shapes = [(args.params,)] if args.params else llama7b_shapes()
     total = sum(numel(s) for s in shapes)
@@ -451,7 +452,7 @@ def run(args, world, rank, local):
     from fate_llm.algo.fedkseed import _native
     build_id = _native.build_id()
     alt_stream = None
-    if world == 1 and not seed_shard and args.alt_stream == "torch_rocm":
+    if world == 1 and not seed_shard and args.alt_stream == "torch_rocm" and not rocm:
         alt_stream = alt_stream_leg(codec, views, ks, kv, wd, total, build_id, max(1, args.alt_stream_steps))
 
     hd = None
@@ -475,7 +476,9 @@ def run(args, world, rank, local):
     rank_seeds = len(ks) * (rank + 1) // world - len(ks) * rank // world if seed_shard else len(ks)
     seeds_per_launch = rank_seeds * n_steps_prof / n_apply
     units = rank_params * seeds_per_launch  # seed*param updates per launch
-    pmc = load_pmc_summary(wd)
+    # the dominant kernel's counters: the slice kernel (torch_cpu), or the torch_rocm stream's
+    # fks_philox_vec_kernel (profiled at wd 0.0 only)
+    pmc = (load_pmc_summary(name=PMC_SUMMARY_PHX) if wd == 0.0 else {}) if rocm else load_pmc_summary(wd)
     lane_ops = pmc.get("valu_lane_ops_per_seed_param")
     valu = None
     withheld = None
@@ -496,7 +499,7 @@ def run(args, world, rank, local):
                 "traffic": (round(pmc["hbm_bytes_per_param_per_launch"] * rank_params)
                             if pmc.get("hbm_bytes_per_param_per_launch") else None),
                 "traffic_unit": "HBM bytes per launch",
-                "kernel": "fks_apply_bs_kernel", "launches": prof.n_apply,
+                "kernel": "fks_philox_vec_kernel" if rocm else "fks_apply_bs_kernel", "launches": prof.n_apply,
                 "avg_launch_ms": round(prof.apply_ms / n_apply, 3),
                 "units_per_launch": units, "lane_ops_per_unit": round(lane_ops, 3),
                 "build_id": build_id,
@@ -543,10 +546,12 @@ def run(args, world, rank, local):
                     "reconstruct, no collective)") if weak else
                    f"{world}xMI355X: 7B-param bf16 buffer, K=4096 seeds, element-sharded (bit-exact, no collective)",
                    "params": total, "k": args.k, "k_nonzero": len(ks), "tensors": len(shapes),
-                   "lr": 1e-5, "weight_decay": wd, "stream": "torch_cpu",
+                   "lr": 1e-5, "weight_decay": wd, "stream": args.stream,
                    "stream_note": ("value draws torch's CPU-generator stream (the oracle-pinned one; a reference "
                                    "client training on the CPU, FKS_STREAM_MODE=torch_cpu); the drop-in's default "
-                                   "on a GPU ('auto') draws torch_rocm, timed as alt_stream"),
+                                   "on a GPU ('auto') draws torch_rocm, timed as alt_stream") if not rocm else
+                                  ("value draws torch's HIP-device generator stream (torch_rocm: the drop-in's "
+                                   "default on a GPU, a reference client whose model sits on the GPU)"),
                    "parallelism": (f"seed-shard{world}" if seed_shard else
                                    f"client-per-gpu{world}" if weak else f"element-shard{world}")},
         "roofline": valu if valu else hbm,
@@ -593,6 +598,9 @@ def main():
                     help="N = 1: one more timed reconstruct drawing the torch_rocm stream (a reference client "
                          "whose model sits on the GPU), with its kernel's VALU roofline")
     ap.add_argument("--alt-stream-steps", type=int, default=3, help="timed steps of the torch_rocm leg (median)")
+    ap.add_argument("--stream", choices=("torch_cpu", "torch_rocm"), default="torch_cpu",
+                    help="the z stream `value` draws (default torch_cpu, the oracle-pinned stream; torch_rocm is the "
+                         "drop-in's default on a GPU, timed beside it as alt_stream)")
     ap.add_argument("--no-hd", dest="hd", action="store_false",
                     help="N = 1: skip the host -> device -> host legs (H2D + reconstruct + D2H, both streams)")
     ap.add_argument("--cpu-budget", type=float, default=24.0)
