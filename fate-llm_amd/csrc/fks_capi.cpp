@@ -167,7 +167,7 @@ void validate(const fks_tensor* t, int nt) {
     const size_t es = elem_size(x.dtype);
     if (x.numel > 0 && (!x.data || ((uintptr_t)x.data % es) != 0))
       throw Error(-FKS_EINVAL, "tensor " + std::to_string(i) + ": null or misaligned data pointer");
-    if (x.flags & ~(FKS_HAS_WD | FKS_FROZEN | FKS_STREAM_ROCM))
+    if (x.flags & ~(FKS_HAS_WD | FKS_FROZEN | FKS_STREAM_ROCM | FKS_FRESH))
       throw Error(-FKS_EINVAL, "tensor " + std::to_string(i) + ": unknown flags");
     if ((x.flags & FKS_STREAM_ROCM) != (t[0].flags & FKS_STREAM_ROCM))
       throw Error(-FKS_EINVAL, "tensor " + std::to_string(i) + ": every tensor of a call must use the same z stream");
@@ -1013,8 +1013,12 @@ void phx_geometry(const fks_tensor* t, int nt, const double* scales, PhxPlan* P,
       x.dtype = t[i].dtype;
       x.lr = t[i].lr;
       x.wd = t[i].wd;
-      x.flags = (t[i].flags & FKS_HAS_WD) | ((x.ptr % 16u) == 0 ? kPhxP16 : 0u) |
-                (((uint64_t)start * es) % 16u == 0 ? kPhxFresh16 : 0u);
+      const bool fresh16 = ((uint64_t)start * es) % 16u == 0;
+      // the alignment of the p the call's first wd * p reads in the reference: this buffer's,
+      // or (FKS_FRESH) that of the tensor an earlier reference step rebound param.data to
+      const bool wd16 = (t[i].flags & FKS_FRESH) ? fresh16 : (x.ptr % 16u) == 0;
+      x.flags = (t[i].flags & FKS_HAS_WD) | ((x.ptr % 16u) == 0 ? kPhxP16 : 0u) | (fresh16 ? kPhxFresh16 : 0u) |
+                (wd16 ? kPhxWdP16 : 0u);
       x.ps = scales ? (float)scales[i] : 0.0f;
       tab.push_back(x);
       elem0.push_back(elems - n + start);

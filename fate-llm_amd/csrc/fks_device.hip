@@ -2699,7 +2699,7 @@ __device__ __forceinline__ void phx_seeds(const PhiloxArgs& a, const PhxTensor& 
   // partial last block of the launch, or every element of a launch whose fresh tensors do
   // not start 16-byte aligned (a later 32-bit piece of a tensor past 2^31 bytes)
   bool tail[4] = {false, false, false, false};
-  const bool p16 = (T.flags & kPhxP16) != 0;
+  const bool p16 = (T.flags & kPhxWdP16) != 0;  // the first wd * p's operand, in the reference
   if (DT == FKS_F16) {
     const bool fresh16 = (T.flags & kPhxFresh16) != 0;
 #pragma unroll

@@ -234,6 +234,10 @@ constexpr uint32_t kPhxP16 = 1u << 8;
 // parameter's size (z, g z, the update's temporaries): false only for the later pieces of a
 // tensor past 2^31 bytes, whose 32-bit-indexed launches start mid-tensor
 constexpr uint32_t kPhxFresh16 = 1u << 9;
+// ... and the p the call's first `wd * p` reads in the reference is 16-byte aligned (the
+// buffer itself, or with FKS_FRESH the fresh tensor an earlier reference step rebound
+// param.data to)
+constexpr uint32_t kPhxWdP16 = 1u << 10;
 // torch's elementwise kernels on ROCm (ATen/native/cuda/CUDALoops.cuh): a 2-byte tensor is
 // processed in blocks of 256 threads x 8 elements; a partial last block takes the unrolled path
 constexpr int64_t kTorchHalfBlockWork = 2048;

@@ -93,6 +93,7 @@ class ParamSpec:
     lr: float = 0.0
     weight_decay: Optional[float] = None  # None -> zo_utils.py:52 form (no decay term)
     frozen: bool = False                  # draws its z, is not written
+    fresh: bool = False                   # the reference's param.data is a tensor an earlier step allocated (mark_rebound)
 
 
 def _f32(x: float) -> float:
@@ -134,6 +135,8 @@ class _Batch:
                 flags |= N.HAS_WD
             if sp.frozen:
                 flags |= N.FROZEN
+            if sp.fresh and stream_flag and t.dtype == torch.float16:  # only the torch_rocm f16 chain reads it
+                flags |= N.FRESH
             arr[i].flags = flags
             arr[i].lr = _f32(sp.lr)
             arr[i].wd = _f32(sp.weight_decay) if sp.weight_decay is not None else 0.0
@@ -420,10 +423,12 @@ def jwin_stats():
     return int(h.value), int(m.value)
 
 
-def perturb(tensors: Sequence[torch.Tensor], seed: int, scales, stream_mode=None, leave_generator: bool = True) -> None:
+def perturb(tensors: Sequence[torch.Tensor], seed: int, scales, stream_mode=None, leave_generator: bool = True,
+            fresh: Optional[Sequence[bool]] = None) -> None:
     """p <- p + scale_i*z for every tensor i (scale = scaling_factor*eps of its group, a
-    python double); ``scales`` is one number for all tensors or one per tensor."""
-    specs = [ParamSpec(t) for t in tensors]
+    python double); ``scales`` is one number for all tensors or one per tensor; ``fresh``:
+    ParamSpec.fresh per tensor."""
+    specs = [ParamSpec(t, fresh=bool(fresh[i]) if fresh else False) for i, t in enumerate(tensors)]
     if not specs:
         return
     if isinstance(scales, (int, float)):
@@ -609,6 +614,25 @@ class profile:
         return False
 
 
+def mark_rebound(params) -> None:
+    """Record that the reference would have rebound each parameter's ``param.data`` to a
+    tensor torch allocated (zo_utils.py:49, optimizer.py:173: every update and perturbation
+    assigns a new tensor), which the drop-in's in-place update does not do: the next call's
+    first ``wd * p`` then reads that fresh, 16-byte-aligned tensor in the reference, whatever
+    the alignment of the buffer here (ParamSpec.fresh, FKS_FRESH; it decides an f16 rounding
+    on the torch_rocm stream).  Keyed on the buffer's address: a parameter whose .data the
+    caller rebinds starts over."""
+    for p in params:
+        try:
+            p._fks_rebound_ptr = p.data_ptr()
+        except (AttributeError, RuntimeError):  # an object that takes no attributes: no record
+            pass
+
+
+def is_rebound(p) -> bool:
+    return getattr(p, "_fks_rebound_ptr", None) == p.data_ptr()
+
+
 def resolve_groups(param_groups: List[dict], lr=None, weight_decay=None) -> List[ParamSpec]:
     """zo_utils.py:43-46: walk the groups in order; lr / weight_decay are re-bound from
     each group only while still None -- so the first group's values stick for all
@@ -619,7 +643,8 @@ def resolve_groups(param_groups: List[dict], lr=None, weight_decay=None) -> List
         lr = group["lr"] if lr is None else lr
         for p in group["params"]:
             specs.append(ParamSpec(p.data, lr=float(lr) if lr is not None else 0.0,
-                                   weight_decay=None if weight_decay is None else float(weight_decay)))
+                                   weight_decay=None if weight_decay is None else float(weight_decay),
+                                   fresh=is_rebound(p)))
     return specs
 
 

@@ -104,6 +104,7 @@ class ZerothOrderOptimizer(RandomWalkOptimizer):
         torch.manual_seed(directional_derivative_seed)
         scales = [1.0 * group["eps"] for group in self.param_groups for _ in group["params"]]
         codec.perturb_step(specs, directional_derivative_seed, scales, v, value_is_tensor=is_tensor, update=True)
+        codec.mark_rebound(p for group in self.param_groups for p in group["params"])
         return g, loss_right, loss_left
 
     # loss dtypes whose g reaches the kernels exactly as an f32 (then rounded to each
@@ -135,6 +136,7 @@ class ZerothOrderOptimizer(RandomWalkOptimizer):
         specs = codec.resolve_groups(self.param_groups)
         scales = [1.0 * group["eps"] for group in self.param_groups for _ in group["params"]]
         codec.perturb_step_device(specs, seed, scales, g, ok)
+        codec.mark_rebound(p for group in self.param_groups for p in group["params"])
         return torch.where(ok, g, torch.full_like(g, math.nan)), loss_right, loss_left
 
     def _fusable(self) -> bool:
@@ -145,14 +147,16 @@ class ZerothOrderOptimizer(RandomWalkOptimizer):
         """p <- p + scaling_factor*eps*z for every parameter that requires grad; frozen
         parameters draw no z (their stream slot is skipped, as in the reference)."""
         torch.manual_seed(directional_derivative_seed)
-        tensors, scales = [], []
+        tensors, scales, params = [], [], []
         for group in self.param_groups:
             scale = scaling_factor * group["eps"]  # python double, cast to fp32 at the multiply
             for p in group["params"]:
                 if p.requires_grad:
                     tensors.append(p.data)
                     scales.append(scale)
-        codec.perturb(tensors, directional_derivative_seed, scales)
+                    params.append(p)
+        codec.perturb(tensors, directional_derivative_seed, scales, fresh=[codec.is_rebound(p) for p in params])
+        codec.mark_rebound(params)  # optimizer.py:173 rebinds param.data
 
 
 class KSeedZerothOrderOptimizer(ZerothOrderOptimizer):

@@ -28,13 +28,29 @@ def probability_from_amps(amps: List[List[float]], clip):
     return ((amp - lo) / (hi - lo + 1e-10)).softmax(0)
 
 
-def _value_kind(value, specs=()):
+def _value_kind(value, specs=(), stream_mode=None):
     """(g as a python float, whether it is a tensor): a tensor g is cast to each
     parameter's dtype by the reference's ``g * z`` (zo_utils.py:49).  A 1-element tensor
     that is not 0-dim takes part in type promotion and broadcasting as a dimensioned
     tensor: that is the same update when the promoted dtype is the parameter's own and
     the parameter has a dimension; otherwise the reference rebinds ``param.data`` to a
-    tensor of another dtype or shape, which an in-place update cannot be -- raised."""
+    tensor of another dtype or shape, which an in-place update cannot be -- raised.
+
+    Where z lives decides the cast: on the CPU (the torch_cpu stream) TensorIterator
+    promotes the 0-dim g to the parameter dtype before the f32 multiply; with z on a GPU
+    (the torch_rocm stream) a 0-dim g on the GPU is cast the same way (the kernel's
+    dynamic-cast load), but a 0-dim g on the CPU is a "CPU scalar" whose f32 value enters
+    the kernel unrounded (gpu_kernel_with_scalars: scalar_value<opmath_t>) -- the same
+    multiply as a python number -- and a dimensioned CPU g is torch's device-mismatch
+    error."""
+    if isinstance(value, torch.Tensor) and value.device.type == "cpu" and specs:
+        dev = specs[0].tensor.device
+        if dev.type == "cuda" and codec.resolve_stream_mode(dev, stream_mode) == "torch_rocm":
+            if value.dim() != 0:
+                raise RuntimeError("Expected all tensors to be on the same device, but found at least two devices, "
+                                   f"{dev} and cpu! (a {tuple(value.shape)} directional_derivative_value on the CPU "
+                                   "times z on the GPU, zo_utils.py:49)")
+            return float(value.item()), False
     if isinstance(value, torch.Tensor):
         if value.dim() != 0:
             if value.numel() != 1:
@@ -71,6 +87,7 @@ def directional_derivative_step(
     specs = codec.resolve_groups(param_groups, lr=lr, weight_decay=weight_decay)
     v, is_tensor = _value_kind(directional_derivative_value, specs)
     codec.directional_step(specs, [directional_derivative_seed], [v], value_is_tensor=is_tensor)
+    codec.mark_rebound(p for g in param_groups for p in g["params"])  # zo_utils.py:49 rebinds param.data
     return directional_derivative_value
 
 
@@ -89,6 +106,7 @@ def reconstruct_(param_groups: List[dict], seeds: Sequence[int], values: Sequenc
     # torch's generators end where the last applied seed's draws leave them (codec._leave).
     codec.directional_step(specs, [s for s, _ in keep], [g for _, g in keep], value_is_tensor=False,
                            cache_windows=True)
+    codec.mark_rebound(p for g in param_groups for p in g["params"])
     return len(keep)
 
 

@@ -66,6 +66,11 @@ extern "C" {
                            a GPU draws (zo_utils.py:47 and optimizer.py:170-172 draw on
                            param.data.device).  Without it: torch's CPU generator (mt19937 +
                            normal_fill).  Every tensor of one call must agree. */
+#define FKS_FRESH 8u    /* FKS_STREAM_ROCM, f16: in the reference, this parameter's param.data is a
+                           tensor torch allocated in an earlier step (zo_utils.py:49 and
+                           optimizer.py:173 rebind it), so the call's first `wd * p` reads 16-byte
+                           aligned data and takes torch's vectorized path, whatever the alignment of
+                           the buffer the drop-in updates in place.  Without it: the buffer's own. */
 
 /* error codes (negated) */
 #define FKS_EINVAL 22
@@ -77,7 +82,7 @@ typedef struct fks_tensor {
   void* data;      /* device pointer, contiguous, numel elements of dtype        */
   int64_t numel;   /* >= 0                                                        */
   int32_t dtype;   /* FKS_F32 / FKS_BF16 / FKS_F16                                */
-  uint32_t flags;  /* FKS_HAS_WD | FKS_FROZEN                                     */
+  uint32_t flags;  /* FKS_HAS_WD | FKS_FROZEN | FKS_STREAM_ROCM | FKS_FRESH        */
   float lr;        /* fp32(lr) as the reference's opmath sees it                   */
   float wd;        /* fp32(weight_decay)                                           */
 } fks_tensor;

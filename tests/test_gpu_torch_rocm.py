@@ -356,3 +356,58 @@ def test_tensor_tables_in_and_out_of_lds(nt):
     torch.cuda.synchronize()
     for i, (a, b) in enumerate(zip(got, ref)):
         _assert_same(a, b, f"tensor {i}")
+
+
+def test_f16_unaligned_view_later_calls_read_a_fresh_tensor(monkeypatch):
+    """The reference rebinds param.data to a tensor torch allocates at every update and
+    perturbation (zo_utils.py:49, optimizer.py:173), so from a parameter's second call on,
+    the first seed's wd * p reads a 16-byte-aligned tensor and takes torch's vectorized path
+    (two roundings of an f16 product), even when the parameter started as an unaligned view;
+    the drop-in updates the view in place and carries that as ParamSpec.fresh / FKS_FRESH
+    (codec.mark_rebound).  Three directional_derivative_step calls and an unfused
+    zeroth-order step (a frozen tensor in the groups) on an f16 view at element offset 1,
+    wd 0.01, against the reference's calls on the device.  With the record switched off the
+    drop-in takes the single rounding there and differs -- the case is exercised.  The
+    zeroth-order step's losses are CPU tensors, so its g is a CPU scalar: torch multiplies
+    its f32 value into z on the GPU without casting it to f16 first (zo_utils._value_kind)."""
+    from fate_llm.algo.fedkseed import codec, zo_utils
+    from fate_llm.algo.fedkseed.optimizer import ZerothOrderOptimizer
+    dev = _dev()
+    n, off = 3_000_001, 1
+    gen = torch.Generator(dev).manual_seed(21)
+    buf = (torch.randn(n + off + 64, device=dev, generator=gen) * 0.05).to(torch.float16)
+    frozen0 = (torch.randn(777, device=dev, generator=gen) * 0.05).to(torch.float16)
+
+    def run(record):
+        if not record:
+            monkeypatch.setattr(codec, "is_rebound", lambda p: False)
+        ref_buf, got_buf = buf.clone(), buf.clone()
+        ref = [torch.nn.Parameter(ref_buf[off:off + n]), torch.nn.Parameter(frozen0.clone(), requires_grad=False)]
+        got = [torch.nn.Parameter(got_buf[off:off + n]), torch.nn.Parameter(frozen0.clone(), requires_grad=False)]
+        assert got[0].data_ptr() % 16 != 0
+        # g z of the size of wd p (|g| ~ 1e-3), so that wd p's rounding shows in t = g z + wd p,
+        # and lr 0.1, so that lr t shows in p
+        rg = [{"params": ref, "lr": 0.1, "weight_decay": 0.01, "eps": 1e-3}]
+        gg = [{"params": got, "lr": 0.1, "weight_decay": 0.01, "eps": 1e-3}]
+        codec.set_stream_mode("torch_rocm")
+        try:
+            for seed, v in [(5, 2e-3), (6, -1.5e-3), (7, 1e-3)]:
+                R.directional_derivative_step(rg, seed, v)
+                zo_utils.directional_derivative_step(gg, seed, v)
+            opt = ZerothOrderOptimizer(gg, lr=0.1, eps=1e-3, weight_decay=0.01, grad_clip=0.0)
+
+            def closure_on(ps):  # a CPU loss: the host path, g a CPU scalar (zo_utils._value_kind)
+                return lambda: ps[0].detach()[:4096].float().sum().cpu() * 1e-6
+
+            R.zeroth_order_step(rg, 99, closure_on(ref), 1e-3)
+            opt.zeroth_order_step(99, closure_on(got))
+        finally:
+            codec.set_stream_mode("torch_cpu")
+            monkeypatch.undo()
+        torch.cuda.synchronize()
+        return got[0].detach(), ref[0].detach()
+
+    got, ref = run(record=True)
+    _assert_same(got, ref, "f16 view at offset 1, later calls")
+    got_off, ref_off = run(record=False)
+    assert not torch.equal(_bits(got_off), _bits(ref_off)), "no midpoint hit: the case is not exercised"

@@ -34,3 +34,27 @@ def test_one_element_that_would_rebind_is_refused(g, p):
 def test_more_than_one_element_is_an_error():
     with pytest.raises(ValueError):
         _value_kind(torch.tensor([0.5, 0.5]), [])
+
+
+def test_cpu_scalar_g_with_z_on_the_gpu_is_not_cast(monkeypatch):
+    """torch_rocm (z on the GPU): a 0-dim CPU g is a CPU scalar, its f32 value enters the
+    multiply unrounded (a python number's kind); a 0-dim GPU g is cast to the parameter
+    dtype; a dimensioned CPU g is torch's device-mismatch error.  (Specs stand in for GPU
+    tensors: only .device and .dtype are read.)"""
+    from fate_llm.algo.fedkseed import codec
+
+    class FakeCuda:
+        device = torch.device("cuda", 0)
+        dtype = torch.bfloat16
+
+        def dim(self):
+            return 1
+
+    specs = [ParamSpec(FakeCuda())]
+    g = torch.tensor(0.1234567)
+    assert _value_kind(g, specs, stream_mode="torch_rocm") == (float(g), False)
+    assert _value_kind(g, specs, stream_mode="torch_cpu") == (float(g), True)
+    monkeypatch.setattr(codec, "_stream_mode", "auto")  # the default resolves to torch_rocm on cuda
+    assert _value_kind(g, specs) == (float(g), False)
+    with pytest.raises(RuntimeError, match="same device"):
+        _value_kind(torch.tensor([0.5]), specs, stream_mode="torch_rocm")
