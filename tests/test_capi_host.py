@@ -180,3 +180,30 @@ def test_cpu_generator_end_matches_torch(layout, seed):
     torch.set_rng_state(ours)
     again = torch.randn(7, dtype=torch.float64), torch.randint(0, 2**31, (5,)), torch.normal(0, 1, (3,))
     assert all(torch.equal(a, b) for a, b in zip(follow, again))
+
+
+@pytest.mark.parametrize("shapes", [[(600_000_000, 0)], [(1_100_000_003, 0), (5, 1)], [(2**30 + 4099, 2), (2**29, 0)]])
+@pytest.mark.parametrize("nshards", [1, 3, 8])
+def test_torch_rocm_pieces_tile_the_tensors(shapes, nshards):
+    """Host geometry of the torch_rocm stream (fks_shard_census, no device: the grid cap
+    falls back to an MI355X's 2,048) for tensors past 2^31 bytes, drawn by torch in
+    32-bit-indexable pieces (phx_geometry): element shards are contiguous runs that tile the
+    concatenation, and every element of every tensor is written exactly once."""
+    N, L = _lib()
+    arr = (N.FksTensor * len(shapes))()
+    for i, (n, d) in enumerate(shapes):
+        arr[i].data = 4096
+        arr[i].numel = n
+        arr[i].dtype = d
+        arr[i].flags = N.STREAM_ROCM
+    total = [0] * len(shapes)
+    lo_expected = 0
+    for r in range(nshards):
+        rng = (ctypes.c_int64 * 2)()
+        wr = (ctypes.c_int64 * len(shapes))()
+        assert L.fks_shard_census(ctypes.addressof(arr), len(shapes), r, nshards, rng, wr) == 0, L.fks_last_error()
+        assert rng[0] == lo_expected and rng[1] >= rng[0]
+        lo_expected = rng[1]
+        total = [a + b for a, b in zip(total, wr)]
+    assert lo_expected == sum(n for n, _ in shapes)
+    assert total == [n for n, _ in shapes]
