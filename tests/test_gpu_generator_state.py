@@ -196,3 +196,38 @@ def test_grid_cap_is_torchs():
     codec.normal_([got], 77, stream_mode="torch_rocm")
     torch.cuda.synchronize()
     assert torch.equal(got.view(torch.int32), want.view(torch.int32))
+
+
+@pytest.mark.parametrize("case", range(12))
+def test_generator_state_fuzz(case):
+    """Random tensor lists (the serial path's < 16 elements with its cached normal, ragged
+    sizes, whole blocks, mixed dtypes), random K and stream: the generator state after
+    codec.directional_step equals the one after the reference's loop, and so do the
+    parameters."""
+    import numpy as np
+
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    rng = np.random.default_rng(700 + case)
+    nt = int(rng.integers(1, 7))
+    sizes = [int(rng.choice([rng.integers(1, 16), rng.integers(16, 3000), 16 * rng.integers(1, 2000)])) for _ in range(nt)]
+    dts = [[torch.float32, torch.bfloat16, torch.float16][int(rng.integers(0, 3))] for _ in range(nt)]
+    stream = ["torch_cpu", "torch_rocm"][case % 2]
+    k = int(rng.integers(1, 40))
+    seeds = [int(s) for s in rng.integers(0, 2**40, k)]
+    vals = [float(v) for v in rng.normal(0, 5, k)]
+    wd = [None, 0.0, 0.01][int(rng.integers(0, 3))]
+    ref_dev = dev if stream == "torch_rocm" else torch.device("cpu")
+    g = torch.Generator().manual_seed(case)
+    init = [(torch.randn(n, generator=g) * 0.05).to(dt) for n, dt in zip(sizes, dts)]
+    ref = [t.to(ref_dev) for t in init]
+    got = [t.to(dev) for t in init]
+    R.reconstruct(ref, seeds, vals, 1e-3, wd)
+    want = _states(dev)
+    torch.manual_seed(12345)
+    codec.directional_step([codec.ParamSpec(t, lr=1e-3, weight_decay=wd) for t in got], seeds, vals,
+                           stream_mode=stream)
+    torch.cuda.synchronize()
+    _assert_states(_states(dev), want, f"case {case} {stream} sizes {sizes}")
+    for i, (a, b) in enumerate(zip(got, ref)):
+        _same(a, b, f"case {case} tensor {i}")
