@@ -162,3 +162,46 @@ def test_c3_two_processes_gloo_on_cuda(dtype):
         assert applied == len(keep)
         w = np.uint16 if got.itemsize == 2 else np.uint32
         assert np.array_equal(got.view(w), ref.view(w)), f"rank {rank}: {int((got.view(w) != ref.view(w)).sum())} differ"
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("wd", [None, 0.01])
+def test_c3_k4096_deviation_torch_rocm(dtype, wd):
+    """The same measurement on the default stream (torch_rocm): the reference's path is its
+    own loop as torch ops on the device (oracle/torch_replica.py), exact arithmetic the K
+    steps in float64 on the same device z; the variant draws the same z
+    (fks_philox_vec_kernel<kModeDelta>).  Reported, not asserted beyond sanity."""
+    from fate_llm.algo.fedkseed import codec, zo_utils
+    from oracle import torch_replica as R
+    dev = _dev()
+    dt = getattr(torch, dtype)
+    n, k, lr = 65536, 4096, 1e-5
+    p0 = (torch.randn(n, generator=torch.Generator().manual_seed(21)) * 0.02).to(dt).to(dev)
+    seeds, vals = _seeds(k, seed=22)
+    for i in range(0, k, 100):
+        vals[i] = 0.0
+    ref = [p0.clone()]
+    R.reconstruct(ref, seeds, vals, lr, wd)
+    exact = p0.double()
+    lr32, wd32 = float(np.float32(lr)), (None if wd is None else float(np.float32(wd)))
+    for s, g in zip(seeds, vals):
+        if g == 0.0:
+            continue
+        torch.manual_seed(s)
+        z = torch.normal(mean=0, std=1, size=(n,), device=dev, dtype=dt).double()
+        exact = exact - lr32 * (float(np.float32(g)) * z + (wd32 * exact if wd32 is not None else 0.0))
+    p = torch.nn.Parameter(p0.clone())
+    codec.set_stream_mode("torch_rocm")
+    try:
+        zo_utils.reconstruct_seed_sharded_([{"params": [p], "lr": 0.0, "weight_decay": 0.0}], seeds, vals, lr=lr,
+                                           weight_decay=wd)
+    finally:
+        codec.set_stream_mode("torch_cpu")
+    torch.cuda.synchronize()
+    got, rf, ex = p.detach().double().cpu().numpy(), ref[0].double().cpu().numpy(), exact.cpu().numpy()
+    r = {"variant_vs_reference": _rel(got, rf), "reference_vs_exact": _rel(rf, ex), "variant_vs_exact": _rel(got, ex)}
+    RESULTS[f"torch_rocm {dtype} wd={wd}"] = r
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "c3_deviation_rocm.json"), "w") as f:
+        json.dump({k_: v for k_, v in RESULTS.items() if k_.startswith("torch_rocm")}, f, indent=1)
+    assert r["variant_vs_exact"] < 1e-2 and r["reference_vs_exact"] < 0.2
