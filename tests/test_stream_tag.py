@@ -254,3 +254,21 @@ def test_arbiter_declares_the_learnt_stream_to_later_rounds(setting):
     setting("auto")
     arb, errors = _federation(["cuda:0"], rounds=2)
     assert not errors and arb.ctx.stream_grid == 2048
+
+
+def test_grid_field_edge_cases():
+    """A torch_rocm record whose grid field is cut off, and a grid flag on a record that is
+    not torch_rocm, are malformed; an untagged reference record still decodes unchanged."""
+    import struct
+    cands = [3, 7]
+    hist = {3: [0.5], 7: []}
+    rec = W.encode_history(hist, cands, "torch_rocm", 2048)
+    with pytest.raises(W.WireFormatError):
+        W.decode_history(rec[:W._HEADER.size + 2], cands)  # the u32 cap cut in half
+    magic, version, kind, flags, count = W._HEADER.unpack_from(rec, 0)
+    bad = W._HEADER.pack(magic, version, kind, (flags & ~W._F_STREAM_ROCM), count) + rec[W._HEADER.size:]
+    with pytest.raises(W.WireFormatError):
+        W.decode_history(bad, cands)  # grid flag on a torch_cpu record
+    plain = W.encode_history(hist, cands)
+    assert W.decode_history(plain, cands) == hist
+    assert struct.unpack_from("<I", rec, W._HEADER.size)[0] == 2048
