@@ -167,14 +167,18 @@ void validate(const fks_tensor* t, int nt) {
     const size_t es = elem_size(x.dtype);
     if (x.numel > 0 && (!x.data || ((uintptr_t)x.data % es) != 0))
       throw Error(-FKS_EINVAL, "tensor " + std::to_string(i) + ": null or misaligned data pointer");
-    if (x.flags & ~(FKS_HAS_WD | FKS_FROZEN | FKS_STREAM_ROCM | FKS_FRESH))
+    if (x.flags & ~(FKS_HAS_WD | FKS_FROZEN | FKS_STREAM_ROCM | FKS_FRESH | FKS_LIBM))
       throw Error(-FKS_EINVAL, "tensor " + std::to_string(i) + ": unknown flags");
-    if ((x.flags & FKS_STREAM_ROCM) != (t[0].flags & FKS_STREAM_ROCM))
+    if ((x.flags & (FKS_STREAM_ROCM | FKS_LIBM)) != (t[0].flags & (FKS_STREAM_ROCM | FKS_LIBM)))
       throw Error(-FKS_EINVAL, "tensor " + std::to_string(i) + ": every tensor of a call must use the same z stream");
+    if ((x.flags & FKS_STREAM_ROCM) && (x.flags & FKS_LIBM))
+      throw Error(-FKS_EINVAL, "tensor " + std::to_string(i) + ": FKS_LIBM is a flavour of the CPU generator's stream");
   }
 }
 
 bool rocm_stream(const fks_tensor* t, int nt) { return nt > 0 && (t[0].flags & FKS_STREAM_ROCM) != 0; }
+// fp32 z of the CPU stream from normal_fill_16<float> with glibc's functions (kDtF32Libm)
+bool libm_flavour(const fks_tensor* t, int nt) { return nt > 0 && (t[0].flags & FKS_LIBM) != 0; }
 
 // Chunk plan: MT blocks [chunk_block[c], chunk_block[c+1]) per workgroup.
 struct Plan {
@@ -1203,6 +1207,7 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
     return;
   }
   const bool small = k <= kSmallK;
+  const bool libm = libm_flavour(t, nt);
   std::lock_guard<std::mutex> lk(g_cache_mu);  // no eviction while this call uses its entry
   const CachedPlan* C = get_plan(t, nt, tensor_scales, delta_base, shard, nshards, small);
   if (!C->have_reg && !C->have_irr) return;
@@ -1379,7 +1384,8 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
         aa.nchunks = C->Z.reg_chunks;
         aa.nseeds = nb;
         aa.mode = mode == kModeUpdate ? C->wd_mode[d] : mode;  // weight-decay select specialised away
-        check(timed(0, stream, [&] { return launch_apply(d, aa, stream); }), "fks_apply_kernel");
+        const int dd = (d == FKS_F32 && libm) ? kDtF32Libm : d;
+        check(timed(0, stream, [&] { return launch_apply(dd, aa, stream); }), "fks_apply_kernel");
       }
     }
     if (C->have_irr) {
@@ -1405,6 +1411,7 @@ void run(const fks_tensor* t, int nt, const uint64_t* seeds, const double* value
       ia.nchunks = C->Z.irr_chunks;
       ia.nseeds = nb;
       ia.mode = mode;
+      ia.libm = libm ? 1 : 0;
       check(timed(0, stream, [&] { return launch_irregular(ia, stream); }), "fks_irregular_kernel");
     }
   }

@@ -203,6 +203,11 @@ struct Traits<FKS_F16> {
   __device__ static float rnd(float x) { return rhf(x); }
 };
 
+// fp32 tensors of the libm flavour (kDtF32Libm): fp32 in every respect but their z
+template <>
+struct Traits<kDtF32Libm> : Traits<FKS_F32> {};
+constexpr bool is_f32(int dt) { return dt == FKS_F32 || dt == kDtF32Libm; }
+
 // One parameter through one seed.  zo_utils.py:49 (has_wd) / :52 ; optimizer.py:173
 // (perturb: p + ps*z, ps = f32(scaling_factor * eps)).
 // Each statement is one torch op rounded to the parameter dtype (fp32 opmath).
@@ -230,7 +235,7 @@ __device__ __forceinline__ float apply_one(float p, float z, float g, float lr, 
 template <int DT>
 __device__ __forceinline__ float dev_value_g(const float* v) {
   const float g = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v[0])));
-  return DT == FKS_F32 ? g : Traits<DT>::rnd(g);
+  return is_f32(DT) ? g : Traits<DT>::rnd(g);
 }
 __device__ __forceinline__ bool dev_value_apply(const float* v) {
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v[1]))) != 0.0f;
@@ -980,6 +985,34 @@ __device__ __forceinline__ void z_pair_f32_raw(uint32_t r1, uint32_t r2, float& 
   z2 = __fmaf_rn(radius, s, 0.0f);
 }
 
+// The libm flavour of the same pair (kDtF32Libm; normal_fill_16<float>,
+// DistributionTemplates.h:139-149, under ATen's DEFAULT CPU capability): glibc's logf / sinf
+// / cosf in double as fks_libm.h restates them, e_logf.c's 16 {invc, logc} pairs read from
+// LDS at byte `tab`; radius * cos(theta) * std + mean with std 1, mean 0 is one rounding of
+// the product and -0 -> +0, the fma with a +0 addend.
+typedef double f64x2_t __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) f64x2_t lds_f64x2_t;
+constexpr int kLdsLogfBytes = 16 * 16;
+__device__ __forceinline__ void logf_tab_fill(uint32_t tab, int tid, int nthreads) {
+  for (int i = tid; i < 16; i += nthreads)
+    *(lds_f64x2_t*)(size_t)(tab + 16u * (uint32_t)i) = (f64x2_t){fks_libm::kLogfTab[i][0], fks_libm::kLogfTab[i][1]};
+}
+__device__ __forceinline__ void z_pair_f32_libm(uint32_t tab, uint32_t r1, uint32_t r2, float& z1, float& z2) {
+  u32x2_t w;
+  w.x = r1;
+  w.y = r2;
+  const u32x2_t t = temper_pair_u24(w);
+  const float u1 = 1.0f - (float)t.x * (1.0f / 16777216.0f);  // 1 - data[j]
+  const float u2 = (float)t.y * (1.0f / 16777216.0f);         // data[j + 8]
+  const f64x2_t e = *(const lds_f64x2_t*)(size_t)(tab + 16u * (uint32_t)fks_libm::logf_index(u1));
+  const float radius = radius_sqrt(-2.0f * fks_libm::logf_core(u1, e.x, e.y));
+  const float theta = (float)(6.283185307179586 * (double)u2);  // 2.0f * c10::pi<double> * u2
+  float s, c;
+  fks_libm::sincosf_glibc(theta, s, c);
+  z1 = __fmaf_rn(radius, c, 0.0f);
+  z2 = __fmaf_rn(radius, s, 0.0f);
+}
+
 // The same z pairs for TWO seeds at once (the fp32 19-seed kernel's full passes): every
 // float operation of cephes_logf / the radius / cephes_sincosf_nonneg runs on the two
 // seeds' values as one packed f32 instruction (v_pk_mul/add/fma_f32: per element the same
@@ -1152,6 +1185,8 @@ template <int DT>
 __device__ __forceinline__ void z_pair(const uint8_t* lds, uint32_t r1, uint32_t r2, float& z1, float& z2) {
   if constexpr (DT == FKS_F32) {
     z_pair_f32_raw(r1, r2, z1, z2);
+  } else if constexpr (DT == kDtF32Libm) {  // the logf table at `lds` (kernels of this dtype: LDS 0)
+    z_pair_f32_libm((uint32_t)(size_t)(const __attribute__((address_space(3))) uint8_t*)lds, r1, r2, z1, z2);
   } else {
     // normal_fill_16<BFloat16>: z = bf16(R[a] * C[b]) * 1 + 0 (std, mean).  R*C is exact
     // in f32 (8-bit x 8-bit significands) and fma(R, C, +0) turns -0 into +0 like "+ mean".
@@ -1348,6 +1383,8 @@ __global__ __launch_bounds__(DB ? kDbThreads : kApplyThreads,
       reinterpret_cast<float*>(lds)[i] = c_tab_bf16[i];
       tabCS[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
     }
+  } else if constexpr (DT == kDtF32Libm) {
+    logf_tab_fill(0u, tid, DB ? kDbThreads : kApplyThreads);
   }
   const int buf1 = DB ? nseeds * kWinBytes : 0;  // DB: the jump windows go to buffer 1
   for (int idx = tid; idx < nseeds * kMtN; idx += (DB ? kDbThreads : kApplyThreads)) {
@@ -1428,7 +1465,7 @@ __global__ __launch_bounds__(DB ? kDbThreads : kApplyThreads,
   // storage: the parameters, or (kModeDelta) the f32 delta buffer the z of dtype DT is
   // accumulated into
   using ST = Traits<MODE == kModeDelta ? FKS_F32 : DT>;
-  constexpr int kEs = (DT == FKS_F32 || MODE == kModeDelta) ? 4 : 2;
+  constexpr int kEs = (is_f32(DT) || MODE == kModeDelta) ? 4 : 2;
   typedef typename ST::Pair Pair;
   struct Slot { uint64_t addr; float lr, wd, ps; uint32_t wdf, on; Pair raw; };
   auto fetch = [&](int64_t b) -> Slot {
@@ -1562,6 +1599,8 @@ __global__ __launch_bounds__(kSm2Threads, kSm2MinWaves) void fks_small2_kernel(A
       reinterpret_cast<float*>(lds)[i] = c_tab_bf16[i];
       reinterpret_cast<float2*>(lds + kLdsCsOff)[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
     }
+  } else if constexpr (DT == kDtF32Libm) {
+    logf_tab_fill(0u, tid, kSm2Threads);
   }
   // the chunk-start windows go to buffer 1, twisted into buffer 0 for block b0
   for (int idx = tid; idx < nseeds * kMtN; idx += kSm2Threads) {
@@ -1608,7 +1647,7 @@ __global__ __launch_bounds__(kSm2Threads, kSm2MinWaves) void fks_small2_kernel(A
   }
 
   using ST = Traits<MODE == kModeDelta ? FKS_F32 : DT>;
-  constexpr int kEs = (DT == FKS_F32 || MODE == kModeDelta) ? 4 : 2;
+  constexpr int kEs = (is_f32(DT) || MODE == kModeDelta) ? 4 : 2;
   constexpr uint32_t kBlockBytes = kMtN * kEs;
   typedef typename ST::Pair Pair;
   const uint32_t joff = (uint32_t)j * kEs;
@@ -2367,9 +2406,14 @@ __device__ __forceinline__ void irr_twist_phase(uint32_t* win, int nseeds, int t
 }
 
 // z pair from two raw words, any dtype (f16 through its 11-bit tables in constant memory)
+constexpr int kIrrLogfOff = kLdsTabBytes + 4 * (kIrrWin * kMaxSeedsPerPass + 16);  // after the wave counters
+static_assert(kIrrLogfOff % 16 == 0, "logf table alignment");
+
 template <int DT>
 __device__ __forceinline__ void irr_z_pair(const uint8_t* lds, uint32_t r1, uint32_t r2, float& z1, float& z2) {
-  if constexpr (DT == FKS_F16) {
+  if constexpr (DT == kDtF32Libm) {
+    z_pair_f32_libm((uint32_t)kIrrLogfOff, r1, r2, z1, z2);
+  } else if constexpr (DT == FKS_F16) {
     const uint32_t a = mt_temper(r1) & 0x7FFu, b = mt_temper(r2) & 0x7FFu;
     z1 = rhf(__fmaf_rn(c_tab_f16[a], c_tab_f16[2048 + b], 0.0f));
     z2 = rhf(__fmaf_rn(c_tab_f16[a], c_tab_f16[4096 + b], 0.0f));
@@ -2389,7 +2433,7 @@ __device__ __forceinline__ void irr_run_lane(const uint8_t* lds, const uint32_t*
     if (on2) p2 = TR::load(R.ptr, e1 + 8);
   }
   const bool has_wd = (R.flags & FKS_HAS_WD) != 0;
-  const float* g = a.g[DT];
+  const float* g = a.g[DT == kDtF32Libm ? FKS_F32 : DT];
   const bool dv = MODE == kModePerturbUpdate && a.gdev;
   const bool upd = dv ? dev_value_apply(a.gdev) : true;
   for (int k = 0; k < a.nseeds; k++) {
@@ -2450,6 +2494,7 @@ __global__ __launch_bounds__(kApplyThreads) void fks_irregular_kernel(IrrArgs a)
       tabCS[i] = make_float2(c_tab_bf16[256 + i], c_tab_bf16[512 + i]);
     }
   }
+  if (a.libm) logf_tab_fill((uint32_t)kIrrLogfOff, tid, kApplyThreads);
   for (int idx = tid; idx < nseeds * kMtN; idx += kApplyThreads) {
     const int k = idx / kMtN, i = idx - k * kMtN;
     win[k * kIrrWin + kIrrCarry + i] = a.states[((size_t)k * a.nchunks + c) * kMtN + i];
@@ -2486,7 +2531,10 @@ __global__ __launch_bounds__(kApplyThreads) void fks_irregular_kernel(IrrArgs a)
         const int64_t e1 = s0 - R.start + r8;
         const int w1 = (int)(s0 - base) + r8;
         switch (R.dtype) {
-          case FKS_F32: irr_run_lane<FKS_F32, MODE>(lds, win, a, R, e1, w1); break;
+          case FKS_F32:
+            if (a.libm) irr_run_lane<kDtF32Libm, MODE>(lds, win, a, R, e1, w1);
+            else irr_run_lane<FKS_F32, MODE>(lds, win, a, R, e1, w1);
+            break;
           case FKS_BF16: irr_run_lane<FKS_BF16, MODE>(lds, win, a, R, e1, w1); break;
           default: irr_run_lane<FKS_F16, MODE>(lds, win, a, R, e1, w1); break;
         }
@@ -3153,6 +3201,14 @@ int launch_apply(int dtype, const ApplyArgs& a, void* stream) {
     case FKS_F32 * 8 + kModePerturbUpdate: return launch_apply_t<FKS_F32, kModePerturbUpdate>(a, stream);
     case FKS_F32 * 8 + kModeWriteZ: return launch_apply_t<FKS_F32, kModeWriteZ>(a, stream);
     case FKS_F32 * 8 + kModeDelta: return launch_apply_t<FKS_F32, kModeDelta>(a, stream);
+    case kDtF32Libm * 8 + kModeUpdate: return launch_apply_t<kDtF32Libm, kModeUpdate>(a, stream);
+    case kDtF32Libm * 8 + kModeUpdateWd: return launch_apply_t<kDtF32Libm, kModeUpdateWd>(a, stream);
+    case kDtF32Libm * 8 + kModeUpdateNoWd: return launch_apply_t<kDtF32Libm, kModeUpdateNoWd>(a, stream);
+    case kDtF32Libm * 8 + kModeUpdateWd0: return launch_apply_t<kDtF32Libm, kModeUpdateWd0>(a, stream);
+    case kDtF32Libm * 8 + kModePerturb: return launch_apply_t<kDtF32Libm, kModePerturb>(a, stream);
+    case kDtF32Libm * 8 + kModePerturbUpdate: return launch_apply_t<kDtF32Libm, kModePerturbUpdate>(a, stream);
+    case kDtF32Libm * 8 + kModeWriteZ: return launch_apply_t<kDtF32Libm, kModeWriteZ>(a, stream);
+    case kDtF32Libm * 8 + kModeDelta: return launch_apply_t<kDtF32Libm, kModeDelta>(a, stream);
     case FKS_BF16 * 8 + kModeUpdate: return launch_apply_t<FKS_BF16, kModeUpdate>(a, stream);
     case FKS_BF16 * 8 + kModeUpdateWd: return launch_apply_t<FKS_BF16, kModeUpdateWd>(a, stream);
     case FKS_BF16 * 8 + kModeUpdateNoWd: return launch_apply_t<FKS_BF16, kModeUpdateNoWd>(a, stream);
@@ -3199,7 +3255,7 @@ int launch_apply_bs(const ApplyBsArgs& a, void* stream) {
 
 template <int MODE>
 static int launch_irregular_m(const IrrArgs& a, void* stream) {
-  const size_t lds = (size_t)kLdsTabBytes + sizeof(uint32_t) * (kIrrWin * (size_t)kMaxSeedsPerPass + 16);
+  const size_t lds = (size_t)kIrrLogfOff + kLdsLogfBytes;  // tables | windows | wave counters | logf table
   static PerDevice attr;
   if (int e = ensure_lds_attr(attr, &fks_irregular_kernel<MODE>, (int)lds)) return e;
   hipLaunchKernelGGL((fks_irregular_kernel<MODE>), dim3((unsigned)a.nchunks), dim3(kApplyThreads), lds,

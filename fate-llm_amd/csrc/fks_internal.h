@@ -117,6 +117,12 @@ constexpr int kJumpXLen = 19937 + 624;  // x[0..20560]: y[i + w] = x[i + w + 1],
 // NaN at load: t = gz, one packed op per element pair and seed fewer
 enum ApplyModeExt : int { kModeUpdateWdPos0 = 8 };
 
+// Device-side dtype of fp32 tensors drawn under FKS_LIBM (ATen's DEFAULT CPU capability):
+// fp32 storage and arithmetic, z from normal_fill_16<float> with glibc's logf / sinf / cosf
+// (fks_libm.h) instead of the AVX2 kernel's Cephes functions.  launch_apply takes it as its
+// dtype; nothing outside the kernels sees it.
+constexpr int kDtF32Libm = 3;
+
 // kModePerturbUpdate: p + ps*z, then the update with the same z (the restore
 // perturbation of zeroth_order_step fused with its directional step)
 // kModeDelta: the seed-sharded variant; z is accumulated into an f32 delta buffer,
@@ -158,6 +164,7 @@ struct IrrArgs {
   int32_t nchunks;
   int32_t nseeds;
   int32_t mode;
+  int32_t libm;                 // fp32 runs draw the libm flavour (FKS_LIBM: kDtF32Libm)
 };
 
 // bf16 slice kernel (fks_apply_bs_kernel): up to 64 seeds per pass; one workgroup per CU

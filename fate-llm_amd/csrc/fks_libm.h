@@ -186,4 +186,95 @@ FKS_HD double sin_or_cos(double theta, bool want_sin) {
   return (q & 2) ? -r : r;
 }
 
+// ---------------------------------------------------------------- fp32, libm flavour
+// Under ATen's DEFAULT CPU capability (ATEN_CPU_CAPABILITY=default, or a host without
+// AVX2) torch fills fp32 tensors of >= 16 elements with normal_fill_16<float>
+// (DistributionTemplates.h:139-149) instead of normal_fill_16_AVX2: per pair
+//   radius = sqrtf(-2 * logf(1 - u1)),  theta = (float)(2 pi_double * u2),
+//   z_j = radius * cosf(theta) * std + mean,  z_{j+8} = radius * sinf(theta) * std + mean
+// with glibc's single-precision logf / sinf / cosf (glibc >= 2.28: sysdeps/ieee754/flt-32
+// e_logf.c, s_sinf.c, s_cosf.c, sincosf.h, from ARM's optimized-routines, evaluated in
+// double).  Restated below for the inputs this path gives them -- logf on u1 = 1 - k 2^-24,
+// sinf / cosf on theta_k, k < 2^24 -- where the special-value arms are unreachable.  The
+// constants are glibc's __logf_data and __sincosf_table (tools/libm_float_consts.py reads
+// them from this image's libm.so.6).  tests/test_libm_float.py compares every one of the
+// 2^24 inputs of each function with the host's glibc, with its FMA dispatch on and off
+// (the two builds agree on these inputs).
+constexpr double kLogfTab[16][2] = {  // {invc, logc}: __logf_data.tab
+    {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2}, {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2},
+    {0x1.49539f0f010b0p+0, -0x1.01eae7f513a67p-2}, {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3},
+    {0x1.30d190c8864a5p+0, -0x1.6574f0ac07758p-3}, {0x1.25e227b0b8ea0p+0, -0x1.1aa2bc79c8100p-3},
+    {0x1.1bb4a4a1a343fp+0, -0x1.a4e76ce8c0e5ep-4}, {0x1.12358f08ae5bap+0, -0x1.1973c5a611cccp-4},
+    {0x1.0953f419900a7p+0, -0x1.252f438e10c1ep-5}, {0x1.0000000000000p+0, 0x0.0p+0},
+    {0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5},  {0x1.ca4b31f026aa0p-1, 0x1.c5e53aa362eb4p-4},
+    {0x1.b2036576afce6p-1, 0x1.526e57720db08p-3},  {0x1.9c2d163a1aa2dp-1, 0x1.bc2860d224770p-3},
+    {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2},  {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2}};
+constexpr double kLogfA0 = -0x1.00ea348b88334p-2, kLogfA1 = 0x1.5575b0be00b6ap-2, kLogfA2 = -0x1.ffffef20a4123p-2,
+                 kLogfLn2 = 0x1.62e42fefa39efp-1;
+// __sincosf_table[0]: 2/pi * 2^24, pi/2, the cosine and sine polynomials ([1] negates the
+// cosine's coefficients, which negates its value exactly)
+constexpr double kScHpiInv = 0x1.45f306dc9c883p+23, kScHpi = 0x1.921fb54442d18p+0, kScC0 = 1.0,
+                 kScC1 = -0x1.ffffffd0c621cp-2, kScC2 = 0x1.55553e1068f19p-5, kScC3 = -0x1.6c087e89a359dp-10,
+                 kScC4 = 0x1.99343027bf8c3p-16, kScS1 = -0x1.555545995a603p-3, kScS2 = 0x1.1107605230bc4p-7,
+                 kScS3 = -0x1.994eb3774cf24p-13;
+
+FKS_HD uint32_t fbits(float x) { return __builtin_bit_cast(uint32_t, x); }
+FKS_HD float from_fbits(uint32_t u) { return __builtin_bit_cast(float, u); }
+
+// e_logf.c's subinterval of a normal x > 0: x = 2^k z, z in [0x3f330000, 2 * that) as bits
+FKS_HD int logf_index(float x) { return (int)(((fbits(x) - 0x3f330000u) >> 19) & 15u); }
+
+// e_logf.c for a normal x > 0 given its table entry (x = 1 takes glibc's early "return 0"
+// arm there and +0 here as well: r = 0, y0 = 0)
+FKS_HD float logf_core(float x, double invc, double logc) {
+  FKS_NO_CONTRACT
+  const uint32_t ix = fbits(x), tmp = ix - 0x3f330000u;
+  const int k = (int32_t)tmp >> 23;
+  const double z = (double)from_fbits(ix - (tmp & 0xff800000u));
+  const double r = z * invc - 1.0;  // log(x) = log1p(z/c - 1) + log(c) + k ln2
+  const double y0 = logc + (double)k * kLogfLn2;
+  const double r2 = r * r;
+  double y = kLogfA1 * r + kLogfA2;
+  y = kLogfA0 * r2 + y;
+  y = y * r2 + (y0 + r);
+  return (float)y;
+}
+
+FKS_HD float logf_glibc(float x) {
+  const int i = logf_index(x);
+  return logf_core(x, kLogfTab[i][0], kLogfTab[i][1]);
+}
+
+// sinf(y) and cosf(y) for 0 <= y < 120: s_sinf.c / s_cosf.c's first two arms.  Their
+// reduce_fast gives n = 0 and x unchanged for y < pi/4, which is the small-argument arm, so
+// one evaluation serves both; only |y| < 2^-12 is special (sin y = y, cos y = 1).
+FKS_HD void sincosf_glibc(float y, float& s, float& c) {
+  FKS_NO_CONTRACT
+  const double x = (double)y;
+  const double r = x * kScHpiInv;                 // reduce_fast without TOINT_INTRINSICS
+  const int n = ((int32_t)r + 0x800000) >> 24;
+  const double xr = x - (double)n * kScHpi;
+  const double xs = ((n + 1) & 2) ? -xr : xr;     // x * sign[n & 3], sign = {1, -1, -1, 1}
+  const double x2 = xs * xs;
+  const double x3 = xs * x2;                      // sinf_poly, even quadrant
+  const double s1 = kScS2 + x2 * kScS3;
+  const double x7 = x3 * x2;
+  const double sp = xs + x3 * kScS1;
+  const float ps = (float)(sp + x7 * s1);
+  const double x4 = x2 * x2;                      // sinf_poly, odd quadrant (table n & 2)
+  const double c2 = kScC3 + x2 * kScC4;
+  const double c1 = kScC0 + x2 * kScC1;
+  const double x6 = x4 * x2;
+  const double cp = c1 + x4 * kScC2;
+  const float pc0 = (float)(cp + x6 * c2);
+  const float pc = (n & 2) ? -pc0 : pc0;
+  const bool odd = (n & 1) != 0;  // sinf takes the cosine polynomial in odd quadrants, cosf in even
+  s = odd ? pc : ps;
+  c = odd ? ps : pc;
+  if ((fbits(y) >> 20) < 0x398u) {  // abstop12(y) < abstop12(0x1p-12f)
+    s = y;
+    c = 1.0f;
+  }
+}
+
 }  // namespace fks_libm

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FKS_LIB_OVERRIDE") or os.path.join(_HERE, "libfks.so")  # override: diagnostics only
 
 F32, BF16, F16 = 0, 1, 2
-HAS_WD, FROZEN, STREAM_ROCM, FRESH = 1, 2, 4, 8
+HAS_WD, FROZEN, STREAM_ROCM, FRESH, LIBM = 1, 2, 4, 8, 16
 VALUE_SCALAR, VALUE_TENSOR = 0, 1
 CHECK_SQRT_DOMAIN = 1
 CHECK_PHILOX_RADIUS = 2

@@ -18,7 +18,9 @@ The z stream (``stream_mode``) is the one the reference draws where its paramete
   torch's grid-stride mapping -- a reference client whose model sits on an MI355X, and
   what the default ``"auto"`` resolves to for every tensor the codec accepts;
 * ``"torch_cpu"``: torch's CPU generator, mt19937 + normal_fill -- a reference client that
-  trains on the CPU (the FedKSeed tutorial's configuration); an explicit choice.
+  trains on the CPU (the FedKSeed tutorial's configuration); an explicit choice.  Its fp32
+  z has two flavours, as torch's CPU kernel has (``cpu_fp32_flavour``): Cephes under
+  ATen's AVX2 / AVX512 capability, glibc's logf / sinf / cosf under DEFAULT.
 
 All parties of one federation must draw the same stream.  The
 process-wide setting comes from ``FKS_STREAM_MODE`` and ``set_stream_mode``: one of the
@@ -71,6 +73,48 @@ def get_stream_mode() -> str:
     return _stream_mode
 
 
+# fp32 tensors of >= 16 elements on the torch_cpu stream: torch's CPU kernel fills them with
+# normal_fill_16_AVX2 (Cephes log / sincos) when ATen dispatches to its AVX2 or AVX512 build
+# and with normal_fill_16<float> (glibc's logf / sinf / cosf) under the DEFAULT capability --
+# ATEN_CPU_CAPABILITY=default, or a host without AVX2 (DistributionTemplates.h:139-149,
+# 195-205).  The reference draws whichever its own process dispatches to, so the flavour is
+# this process's torch's unless FKS_CPU_FP32_FLAVOUR or set_cpu_fp32_flavour names one (a
+# drop-in joining reference clients that run another capability).  bf16 / f16 tensors and
+# tensors of < 16 elements draw the same z either way.
+CPU_FP32_FLAVOURS = ("avx", "libm")
+_cpu_fp32_flavour = os.environ.get("FKS_CPU_FP32_FLAVOUR") or None
+if _cpu_fp32_flavour is not None and _cpu_fp32_flavour not in CPU_FP32_FLAVOURS:
+    raise ValueError(f"FKS_CPU_FP32_FLAVOUR must be one of {CPU_FP32_FLAVOURS}, not {_cpu_fp32_flavour!r}")
+
+
+def set_cpu_fp32_flavour(flavour: Optional[str]) -> None:
+    """"avx", "libm", or None for this process's torch's CPU capability."""
+    global _cpu_fp32_flavour
+    if flavour is not None and flavour not in CPU_FP32_FLAVOURS:
+        raise ValueError(f"cpu fp32 flavour must be one of {CPU_FP32_FLAVOURS} or None, not {flavour!r}")
+    _cpu_fp32_flavour = flavour
+
+
+def cpu_fp32_flavour() -> str:
+    """The fp32 z of the torch_cpu stream: "avx" (normal_fill_16_AVX2) or "libm"
+    (normal_fill_16<float>), per the setting or torch.backends.cpu.get_cpu_capability()."""
+    if _cpu_fp32_flavour is not None:
+        return _cpu_fp32_flavour
+    return "avx" if torch.backends.cpu.get_cpu_capability() in ("AVX2", "AVX512") else "libm"
+
+
+def stream_identity(stream_mode: str, params=None) -> str:
+    """The stream as parties compare it (payload.py): ``stream_mode``, except that a
+    torch_cpu stream whose fp32 z is the libm flavour is "torch_cpu_libm" -- when ``params``
+    (an iterable of tensors, None = assume so) hold an fp32 tensor of >= 16 elements, the
+    only draws the flavour changes."""
+    if stream_mode != "torch_cpu" or cpu_fp32_flavour() != "libm":
+        return stream_mode
+    if params is not None and not any(p.dtype == torch.float32 and p.numel() >= 16 for p in params):
+        return stream_mode
+    return "torch_cpu_libm"
+
+
 def resolve_stream_mode(device=None, stream_mode=None) -> str:
     """The stream a call on tensors of ``device`` draws: ``stream_mode`` if given, else the
     process-wide setting; "auto" is the stream the reference draws on that device
@@ -120,6 +164,8 @@ class _Batch:
                 raise ValueError("FedKSeed codec: all parameters must be on one device")
         self.stream_mode = resolve_stream_mode(self.device, stream_mode)
         stream_flag = N.STREAM_ROCM if self.stream_mode == "torch_rocm" else 0
+        # the CPU stream's fp32 flavour travels on every tensor (the library wants one per call)
+        cpu_flag = N.LIBM if not stream_flag and cpu_fp32_flavour() == "libm" else 0
         arr = (N.FksTensor * max(1, len(self.specs)))()
         for i, sp in enumerate(self.specs):
             t = sp.tensor
@@ -130,7 +176,7 @@ class _Batch:
             arr[i].data = t.data_ptr() if t.numel() else None
             arr[i].numel = t.numel()
             arr[i].dtype = _DTYPES[t.dtype]
-            flags = stream_flag
+            flags = stream_flag | cpu_flag
             if sp.weight_decay is not None:
                 flags |= N.HAS_WD
             if sp.frozen:

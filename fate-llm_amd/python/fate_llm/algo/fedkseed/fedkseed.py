@@ -237,8 +237,11 @@ class ClientTrainer:
     def stream_mode(self) -> str:
         """The z stream this client's reconstruct and local steps draw: the process-wide
         codec setting resolved for the training device (FKS_STREAM_MODE unset = "auto":
-        torch_rocm on an MI355X, what an unmodified reference client there draws)."""
-        return codec.resolve_stream_mode(getattr(self.training_args, "device", None))
+        torch_rocm on an MI355X, what an unmodified reference client there draws), as
+        codec.stream_identity names it ("torch_cpu_libm": the CPU stream under ATen's DEFAULT
+        capability, for a model with fp32 tensors of >= 16 elements)."""
+        mode = codec.resolve_stream_mode(getattr(self.training_args, "device", None))
+        return codec.stream_identity(mode, self.model_0.parameters() if self.model_0 is not None else None)
 
     @property
     def stream_grid(self):

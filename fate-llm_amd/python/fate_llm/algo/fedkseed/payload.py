@@ -77,7 +77,8 @@ _F_SPARSE = 1 << 3        # keys = the candidates: only (index, count) of non-em
 _F_STREAM_TAGGED = 1 << 8
 _F_STREAM_ROCM = 1 << 9
 _F_STREAM_GRID = 1 << 10  # a u32 grid cap follows the header (torch_rocm only)
-STREAMS = ("torch_cpu", "torch_rocm")
+_F_STREAM_LIBM = 1 << 11  # torch_cpu with the libm flavour of fp32 z (codec.stream_identity)
+STREAMS = ("torch_cpu", "torch_cpu_libm", "torch_rocm")
 _GRID = struct.Struct("<I")
 
 _HEADER = struct.Struct("<4sBBHQ")  # magic, version, kind, flags, count
@@ -113,13 +114,20 @@ def _stream_flags(stream_mode: Optional[str], stream_grid: Optional[int] = None)
         if not 0 < int(stream_grid) < 2 ** 32:
             raise WireFormatError(f"stream_grid must be a positive u32, not {stream_grid!r}")
     return (_F_STREAM_TAGGED | (_F_STREAM_ROCM if stream_mode == "torch_rocm" else 0)
+            | (_F_STREAM_LIBM if stream_mode == "torch_cpu_libm" else 0)
             | (_F_STREAM_GRID if stream_grid is not None else 0))
 
 
 def _stream_of(flags: int) -> Optional[str]:
     if not flags & _F_STREAM_TAGGED:
+        if flags & (_F_STREAM_ROCM | _F_STREAM_LIBM | _F_STREAM_GRID):
+            raise WireFormatError("stream bits on an untagged record")
         return None
-    return "torch_rocm" if flags & _F_STREAM_ROCM else "torch_cpu"
+    if flags & _F_STREAM_ROCM:
+        if flags & _F_STREAM_LIBM:
+            raise WireFormatError("the libm flavour belongs to the torch_cpu stream only")
+        return "torch_rocm"
+    return "torch_cpu_libm" if flags & _F_STREAM_LIBM else "torch_cpu"
 
 
 def _grid_bytes(stream_grid: Optional[int]) -> bytes:
@@ -151,8 +159,10 @@ def check_stream(expected: Optional[str], got: Optional[str], what: str, expecte
             f"{what} draws the {describe_stream(got, got_grid)} z stream, this federation draws "
             f"{describe_stream(expected, expected_grid)}: the parties would apply the same (seed, scalar) list "
             "along different directions (zo_utils.py:47 draws on the parameters' device, in a grid of at most "
-            "CUs x threads per CU / 256 blocks); set FKS_STREAM_MODE / codec.set_stream_mode alike on every "
-            "party and train every torch_rocm party on devices of one CU count and partition mode")
+            "CUs x threads per CU / 256 blocks; on the CPU generator, fp32 z follows ATen's CPU capability: "
+            "torch_cpu_libm is ATEN_CPU_CAPABILITY=default); set FKS_STREAM_MODE / codec.set_stream_mode alike on "
+            "every party, train every torch_rocm party on devices of one CU count and partition mode, and every "
+            "torch_cpu party under one CPU capability (FKS_CPU_FP32_FLAVOUR)")
 
 
 def _keys_array(keys: Sequence[int]) -> Tuple[np.ndarray, bool]:

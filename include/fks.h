@@ -71,6 +71,14 @@ extern "C" {
                            optimizer.py:173 rebind it), so the call's first `wd * p` reads 16-byte
                            aligned data and takes torch's vectorized path, whatever the alignment of
                            the buffer the drop-in updates in place.  Without it: the buffer's own. */
+#define FKS_LIBM 16u    /* CPU generator's stream (no FKS_STREAM_ROCM), fp32 tensors of >= 16
+                           elements: z from normal_fill_16<float> with glibc's logf / sinf / cosf,
+                           what torch draws under ATen's DEFAULT CPU capability
+                           (ATEN_CPU_CAPABILITY=default, or a host without AVX2;
+                           DistributionTemplates.h:139-149), instead of normal_fill_16_AVX2's
+                           Cephes functions.  Every tensor of a call carries it or none does;
+                           bf16 / f16 tensors and tensors of < 16 elements draw the same z either
+                           way. */
 
 /* error codes (negated) */
 #define FKS_EINVAL 22
@@ -82,7 +90,7 @@ typedef struct fks_tensor {
   void* data;      /* device pointer, contiguous, numel elements of dtype        */
   int64_t numel;   /* >= 0                                                        */
   int32_t dtype;   /* FKS_F32 / FKS_BF16 / FKS_F16                                */
-  uint32_t flags;  /* FKS_HAS_WD | FKS_FROZEN | FKS_STREAM_ROCM | FKS_FRESH        */
+  uint32_t flags;  /* FKS_HAS_WD | FKS_FROZEN | FKS_STREAM_ROCM | FKS_FRESH | FKS_LIBM */
   float lr;        /* fp32(lr) as the reference's opmath sees it                   */
   float wd;        /* fp32(weight_decay)                                           */
 } fks_tensor;

@@ -5,6 +5,11 @@
 //   libm_check sincos N     -> "bad <count>" then up to 256 "theta mine glibc" hex lines
 //   libm_check z            -> stdin "a b which" (53-bit hex, which 0 = cos, 1 = sin);
 //                              stdout the fp32 bits of the serial-path z, header and glibc
+//   libm_check logf         -> "bad <count>": logf_glibc against logf on all 2^24 u1 = 1 - k 2^-24
+//   libm_check sincosf      -> "bad <count>": sincosf_glibc against sinf / cosf on all 2^24
+//                              theta_k = (float)(2 pi_double k 2^-24)
+//   libm_check consts       -> the header's logf / sincosf constants, one %a per line, in the
+//                              order tools/libm_float_consts.py lists glibc's
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -54,6 +59,36 @@ int main(int argc, char** argv) {
       }
     }
     printf("bad %ld\n", bad);
+    return 0;
+  }
+  if (!strcmp(argv[1], "logf")) {
+    long bad = 0;
+    for (uint32_t k = 0; k < (1u << 24); k++) {
+      const float u1 = 1.0f - (float)k * (1.0f / 16777216.0f);
+      if (fks_libm::fbits(fks_libm::logf_glibc(u1)) != fks_libm::fbits(logf(u1))) bad++;
+    }
+    printf("bad %ld\n", bad);
+    return 0;
+  }
+  if (!strcmp(argv[1], "sincosf")) {
+    long bad = 0;
+    for (uint32_t k = 0; k < (1u << 24); k++) {
+      const float th = (float)(2.0f * 3.14159265358979323846 * (double)((float)k * (1.0f / 16777216.0f)));
+      float s, c;
+      fks_libm::sincosf_glibc(th, s, c);
+      if (fks_libm::fbits(s) != fks_libm::fbits(sinf(th))) bad++;
+      if (fks_libm::fbits(c) != fks_libm::fbits(cosf(th))) bad++;
+    }
+    printf("bad %ld\n", bad);
+    return 0;
+  }
+  if (!strcmp(argv[1], "consts")) {
+    for (int i = 0; i < 16; i++) printf("%a\n%a\n", fks_libm::kLogfTab[i][0], fks_libm::kLogfTab[i][1]);
+    const double rest[] = {fks_libm::kLogfLn2, fks_libm::kLogfA0, fks_libm::kLogfA1, fks_libm::kLogfA2,
+                           fks_libm::kScHpiInv, fks_libm::kScHpi, fks_libm::kScC0, fks_libm::kScC1,
+                           fks_libm::kScS1, fks_libm::kScC2, fks_libm::kScS2, fks_libm::kScC3,
+                           fks_libm::kScS3, fks_libm::kScC4};
+    for (double v : rest) printf("%a\n", v);
     return 0;
   }
   if (!strcmp(argv[1], "z")) {

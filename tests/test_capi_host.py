@@ -140,6 +140,19 @@ def test_invalid_inputs_rejected():
     arr[0].data = 16
     arr[0].dtype = 7
     assert L.fks_workspace_size(ctypes.addressof(arr), 1, 1, ctypes.byref(nbytes)) < 0
+    # FKS_LIBM is a flavour of the CPU generator's stream, one per call
+    arr[0].dtype = N.F32
+    arr[0].flags = N.LIBM | N.STREAM_ROCM
+    assert L.fks_workspace_size(ctypes.addressof(arr), 1, 1, ctypes.byref(nbytes)) < 0
+    assert b"flavour" in L.fks_last_error()
+    two = (N.FksTensor * 2)()
+    for i in range(2):
+        two[i].data = 16
+        two[i].numel = 32
+        two[i].dtype = N.F32
+    two[0].flags = N.LIBM
+    assert L.fks_workspace_size(ctypes.addressof(two), 2, 1, ctypes.byref(nbytes)) < 0
+    assert b"same z stream" in L.fks_last_error()
 
 
 _TORCH_DT = {0: "float32", 1: "bfloat16", 2: "float16"}

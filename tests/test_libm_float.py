@@ -1,0 +1,130 @@
+"""The fp32 libm flavour of the CPU generator's z stream (FKS_LIBM): host-side checks.
+
+* fate-llm_amd/csrc/fks_libm.h's restatement of glibc's logf / sinf / cosf (the source the
+  device build includes, compiled here by g++ with contraction off: tests/libm_check.cpp)
+  equals this host's glibc on EVERY input normal_fill_16<float> gives them -- logf on the
+  2^24 values u1 = 1 - k 2^-24, sinf / cosf on the 2^24 values (float)(2 pi_double k 2^-24)
+  -- with glibc's FMA ifunc variants selected and with them masked off
+  (GLIBC_TUNABLES=glibc.cpu.hwcaps=-AVX2,-FMA,-FMA4: what a host without AVX2 runs);
+* its constants are the ones in this image's libm.so.6 (tools/libm_float_consts.py);
+* the codec picks the flavour from torch's CPU capability, and the wire tag carries it.
+"""
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+NO_FMA = "glibc.cpu.hwcaps=-AVX2,-FMA,-FMA4"
+
+
+@pytest.fixture(scope="module")
+def checker(tmp_path_factory):
+    exe = tmp_path_factory.mktemp("libmf") / "libm_check"
+    subprocess.run(["g++", "-O2", "-ffp-contract=off", "-std=c++17", "-o", str(exe),
+                    str(ROOT / "tests" / "libm_check.cpp"), "-lm"], check=True)
+    return exe
+
+
+def _run(exe, mode, tunables=None):
+    env = dict(os.environ)
+    if tunables:
+        env["GLIBC_TUNABLES"] = tunables
+    return subprocess.run([str(exe), mode], capture_output=True, text=True, check=True, env=env).stdout
+
+
+@pytest.mark.parametrize("tunables", [None, NO_FMA])
+@pytest.mark.parametrize("fn", ["logf", "sincosf"])
+def test_every_input_equals_glibc(checker, fn, tunables):
+    assert _run(checker, fn, tunables).split() == ["bad", "0"]
+
+
+def test_tunables_mask_fma():
+    """The NO_FMA setting does reach glibc's CPU features (so the case above is the non-FMA
+    build): ld.so's diagnostics show FMA (CPUID.1:ECX bit 12) off."""
+    ld = "/lib64/ld-linux-x86-64.so.2"
+    if not os.path.exists(ld):
+        pytest.skip("no x86-64 ld.so")
+
+    def ecx():
+        out = subprocess.run([ld, "--list-diagnostics"], capture_output=True, text=True,
+                             env={**os.environ, "GLIBC_TUNABLES": NO_FMA} if masked else dict(os.environ)).stdout
+        line = [x for x in out.splitlines() if x.startswith("x86.cpu_features.features[0x0].active[0x2]=")]
+        return int(line[0].split("=")[1], 16) if line else None
+
+    masked = False
+    on = ecx()
+    masked = True
+    off = ecx()
+    if on is None or not on & (1 << 12):
+        pytest.skip("this host has no FMA to mask")
+    assert not off & (1 << 12)
+
+
+def test_constants_are_glibcs(checker):
+    sys.path.insert(0, str(ROOT / "tools"))
+    import libm_float_consts
+    libm = "/lib/x86_64-linux-gnu/libm.so.6"
+    if not os.path.exists(libm):
+        pytest.skip("no x86-64 glibc libm")
+    mine = [float.fromhex(x) for x in _run(checker, "consts").split()]
+    assert mine == libm_float_consts.constants(libm)
+
+
+def test_flavour_follows_torch_capability():
+    code = ("import sys; sys.path.insert(0, 'fate-llm_amd/python'); import torch; "
+            "from fate_llm.algo.fedkseed import codec; "
+            "print(torch.backends.cpu.get_cpu_capability(), codec.cpu_fp32_flavour())")
+    env = {k: v for k, v in os.environ.items() if k != "FKS_CPU_FP32_FLAVOUR"}
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, check=True,
+                         env={**env, "ATEN_CPU_CAPABILITY": "default"}).stdout.split()
+    assert out == ["DEFAULT", "libm"]
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, check=True,
+                         env={**env, "ATEN_CPU_CAPABILITY": "default", "FKS_CPU_FP32_FLAVOUR": "avx"}).stdout.split()
+    assert out == ["DEFAULT", "avx"]
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, check=True,
+                         env=env).stdout.split()
+    assert out[1] == ("avx" if out[0] in ("AVX2", "AVX512") else "libm")
+
+
+def test_stream_identity():
+    import torch
+    from fate_llm.algo.fedkseed import codec
+    f32 = [torch.zeros(16)]
+    small = [torch.zeros(15), torch.zeros(64, dtype=torch.bfloat16)]
+    try:
+        codec.set_cpu_fp32_flavour("libm")
+        assert codec.stream_identity("torch_cpu") == "torch_cpu_libm"
+        assert codec.stream_identity("torch_cpu", f32) == "torch_cpu_libm"
+        assert codec.stream_identity("torch_cpu", small) == "torch_cpu"  # no draw the flavour changes
+        assert codec.stream_identity("torch_rocm", f32) == "torch_rocm"
+        codec.set_cpu_fp32_flavour("avx")
+        assert codec.stream_identity("torch_cpu", f32) == "torch_cpu"
+        with pytest.raises(ValueError):
+            codec.set_cpu_fp32_flavour("sse")
+    finally:
+        codec.set_cpu_fp32_flavour(None)
+
+
+def test_wire_tag_carries_the_flavour():
+    from fate_llm.algo.fedkseed import payload as P
+    hist = {5: [1.0, 2.0], 9: []}
+    for mode in ("torch_cpu", "torch_cpu_libm"):
+        got = P.decode_history(P.encode_history(hist, None, stream_mode=mode))
+        assert got == hist and got.stream_mode == mode
+    msg = (False, {"seed_candidates": [5, 9], "seed_probabilities": [0.5, 0.5], "direction_derivative_sum": None})
+    _, kw = P.decode_train_once(P.encode_train_once(msg, stream_mode="torch_cpu_libm"))
+    assert kw["stream_mode"] == "torch_cpu_libm"
+    with pytest.raises(P.StreamMismatchError):
+        P.check_stream("torch_cpu", "torch_cpu_libm", "client 1")
+    P.check_stream("torch_cpu_libm", "torch_cpu_libm", "client 1")
+    with pytest.raises(P.WireFormatError):
+        P.encode_history(hist, None, stream_mode="torch_cpu_libm", stream_grid=2048)
+    # a record claiming both the device stream and the libm flavour is malformed
+    buf = bytearray(P.encode_history(hist, None, stream_mode="torch_rocm"))
+    flags = int.from_bytes(buf[6:8], "little") | (1 << 11)
+    buf[6:8] = flags.to_bytes(2, "little")
+    with pytest.raises(P.WireFormatError):
+        P.decode_history(bytes(buf))

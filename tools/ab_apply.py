@@ -2,7 +2,8 @@
 the in-tree libfks.so).  Each build runs in its own process (FKS_LIB_OVERRIDE) on the
 same workload -- N bf16 params (default 2^28), K seeds (default 95 = 5 full passes),
 wd AB_WD (default 0.01, 'none' for None) -- and prints the average apply/jump launch time per pass (AB_SEEDS seeds per
-launch for the per-seed figure: 19, or 32 for the bf16 slice kernel)."""
+launch for the per-seed figure: 19, or 32 for the bf16 slice kernel).  AB_DT=f32: fp32 params
+(FKS_CPU_FP32_FLAVOUR=libm: the libm flavour's kernel)."""
 import json
 import os
 os.environ.setdefault("FKS_STREAM_MODE", "torch_cpu")  # the CPU-generator stream these measurements use
@@ -31,6 +32,7 @@ for _ in range(3):
     r = p.apply_ms / max(p.n_apply, 1)
     best = r if best is None else min(best, r)
 print(json.dumps({"lib": os.environ.get("FKS_LIB_OVERRIDE", "libfks.so"), "dtype": str(dt), "n": n, "k": k, "wd": wd,
+                  "fp32_flavour": codec.cpu_fp32_flavour(),
                   "apply_ms_per_launch": round(best, 3),
                   "ps_per_seed_param": round(best * 1e9 / (n * int(os.environ.get("AB_SEEDS", "19"))), 3)}), flush=True)
 '''
