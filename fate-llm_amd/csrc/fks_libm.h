@@ -199,7 +199,12 @@ FKS_HD double sin_or_cos(double theta, bool want_sin) {
 // constants are glibc's __logf_data and __sincosf_table (tools/libm_float_consts.py reads
 // them from this image's libm.so.6).  tests/test_libm_float.py compares every one of the
 // 2^24 inputs of each function with the host's glibc, with its FMA dispatch on and off
-// (the two builds agree on these inputs).
+// (the two builds agree on these inputs), in both evaluation forms below: FMA = false is
+// glibc's source order with every product rounded (its non-FMA build); FMA = true fuses each
+// "a * b + c" of the source into one fma, as its FMA build may, and is what the device runs
+// (f64 arithmetic issues at half the f32 rate on gfx950: 7 instead of 11 f64 operations per
+// logf, 14 instead of 21 per sine-cosine pair).  Both forms give glibc's value on every
+// input of the domain -- the final rounding to float absorbs their difference there.
 constexpr double kLogfTab[16][2] = {  // {invc, logc}: __logf_data.tab
     {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2}, {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2},
     {0x1.49539f0f010b0p+0, -0x1.01eae7f513a67p-2}, {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3},
@@ -224,56 +229,81 @@ FKS_HD float from_fbits(uint32_t u) { return __builtin_bit_cast(float, u); }
 // e_logf.c's subinterval of a normal x > 0: x = 2^k z, z in [0x3f330000, 2 * that) as bits
 FKS_HD int logf_index(float x) { return (int)(((fbits(x) - 0x3f330000u) >> 19) & 15u); }
 
+// normal_fill_16<float>'s angle for the 24-bit uniform b: theta = (float)(2.0f *
+// c10::pi<double> * u2) with u2 = b 2^-24, i.e. RN_float(RN_double(2 pi_double * u2)).  The
+// double product equals RN_double((2 pi_double 2^-24) * b) -- a power-of-two scaling, exact
+// in double -- so it is one conversion of b and one multiply (tests/libm_check.cpp "theta")
+FKS_HD float theta_of(uint32_t b) { return (float)((double)b * 0x1.921fb54442d18p-22); }
+
+// a * b + c, fused (FMA) or with the product rounded
+template <bool FMA>
+FKS_HD double mad(double a, double b, double c) {
+  FKS_NO_CONTRACT
+  if constexpr (FMA) return __builtin_fma(a, b, c);
+  return a * b + c;
+}
+
 // e_logf.c for a normal x > 0 given its table entry (x = 1 takes glibc's early "return 0"
 // arm there and +0 here as well: r = 0, y0 = 0)
+template <bool FMA>
 FKS_HD float logf_core(float x, double invc, double logc) {
   FKS_NO_CONTRACT
   const uint32_t ix = fbits(x), tmp = ix - 0x3f330000u;
   const int k = (int32_t)tmp >> 23;
   const double z = (double)from_fbits(ix - (tmp & 0xff800000u));
-  const double r = z * invc - 1.0;  // log(x) = log1p(z/c - 1) + log(c) + k ln2
-  const double y0 = logc + (double)k * kLogfLn2;
+  const double r = mad<FMA>(z, invc, -1.0);  // log(x) = log1p(z/c - 1) + log(c) + k ln2
+  const double y0 = mad<FMA>((double)k, kLogfLn2, logc);
   const double r2 = r * r;
-  double y = kLogfA1 * r + kLogfA2;
-  y = kLogfA0 * r2 + y;
-  y = y * r2 + (y0 + r);
+  double y = mad<FMA>(kLogfA1, r, kLogfA2);
+  y = mad<FMA>(kLogfA0, r2, y);
+  y = mad<FMA>(y, r2, y0 + r);
   return (float)y;
 }
 
+template <bool FMA>
 FKS_HD float logf_glibc(float x) {
   const int i = logf_index(x);
-  return logf_core(x, kLogfTab[i][0], kLogfTab[i][1]);
+  return logf_core<FMA>(x, kLogfTab[i][0], kLogfTab[i][1]);
 }
 
 // sinf(y) and cosf(y) for 0 <= y < 120: s_sinf.c / s_cosf.c's first two arms.  Their
 // reduce_fast gives n = 0 and x unchanged for y < pi/4, which is the small-argument arm, so
-// one evaluation serves both; only |y| < 2^-12 is special (sin y = y, cos y = 1).
+// one evaluation serves both; only |y| < 2^-12 is special (sin y = y, cos y = 1), and for
+// y >= 0 not even that (below).
+template <bool FMA>
 FKS_HD void sincosf_glibc(float y, float& s, float& c) {
   FKS_NO_CONTRACT
   const double x = (double)y;
   const double r = x * kScHpiInv;                 // reduce_fast without TOINT_INTRINSICS
   const int n = ((int32_t)r + 0x800000) >> 24;
-  const double xr = x - (double)n * kScHpi;
-  const double xs = ((n + 1) & 2) ? -xr : xr;     // x * sign[n & 3], sign = {1, -1, -1, 1}
+  const double xr = mad<FMA>(-(double)n, kScHpi, x);
+  // x * sign[n & 3], sign = {1, -1, -1, 1}: the sign bit flipped for n & 3 in {1, 2}
+  const double xs = from_bits(bits(xr) ^ ((uint64_t)((uint32_t)(n + 1) & 2u) << 62));
   const double x2 = xs * xs;
   const double x3 = xs * x2;                      // sinf_poly, even quadrant
-  const double s1 = kScS2 + x2 * kScS3;
+  const double s1 = mad<FMA>(x2, kScS3, kScS2);
   const double x7 = x3 * x2;
-  const double sp = xs + x3 * kScS1;
-  const float ps = (float)(sp + x7 * s1);
+  const double sp = mad<FMA>(x3, kScS1, xs);
+  const float ps = (float)mad<FMA>(x7, s1, sp);
   const double x4 = x2 * x2;                      // sinf_poly, odd quadrant (table n & 2)
-  const double c2 = kScC3 + x2 * kScC4;
-  const double c1 = kScC0 + x2 * kScC1;
+  const double c2 = mad<FMA>(x2, kScC4, kScC3);
+  const double c1 = mad<FMA>(x2, kScC1, kScC0);
   const double x6 = x4 * x2;
-  const double cp = c1 + x4 * kScC2;
-  const float pc0 = (float)(cp + x6 * c2);
-  const float pc = (n & 2) ? -pc0 : pc0;
+  const double cp = mad<FMA>(x4, kScC2, c1);
+  const float pc0 = (float)mad<FMA>(x6, c2, cp);
+  const float pc = from_fbits(fbits(pc0) ^ (((uint32_t)n & 2u) << 30));  // table n & 2: negated
   const bool odd = (n & 1) != 0;  // sinf takes the cosine polynomial in odd quadrants, cosf in even
   s = odd ? pc : ps;
   c = odd ? ps : pc;
-  if ((fbits(y) >> 20) < 0x398u) {  // abstop12(y) < abstop12(0x1p-12f)
-    s = y;
-    c = 1.0f;
+  // |y| < 2^-12 (abstop12(y) < abstop12(0x1p-12f)): glibc returns y and 1.0f.  For y >= 0
+  // that is what the polynomials round to there as well -- sin: y (1 - y^2/6 ...) is within
+  // 2^-26.6 y of y, below half an ulp; cos: 1 - y^2/2 with y^2/2 < 2^-25, below half the
+  // spacing under 1 -- so the fused form drops the arm (the exhaustive checks cover both)
+  if constexpr (!FMA) {
+    if ((fbits(y) >> 20) < 0x398u) {
+      s = y;
+      c = 1.0f;
+    }
   }
 }
 

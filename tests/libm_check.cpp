@@ -5,9 +5,11 @@
 //   libm_check sincos N     -> "bad <count>" then up to 256 "theta mine glibc" hex lines
 //   libm_check z            -> stdin "a b which" (53-bit hex, which 0 = cos, 1 = sin);
 //                              stdout the fp32 bits of the serial-path z, header and glibc
-//   libm_check logf         -> "bad <count>": logf_glibc against logf on all 2^24 u1 = 1 - k 2^-24
-//   libm_check sincosf      -> "bad <count>": sincosf_glibc against sinf / cosf on all 2^24
+//   libm_check logf [fma]   -> "bad <count>": logf_glibc against logf on all 2^24 u1 = 1 - k 2^-24
+//   libm_check sincosf [fma] -> "bad <count>": sincosf_glibc against sinf / cosf on all 2^24
 //                              theta_k = (float)(2 pi_double k 2^-24)
+//                              (fma: the fused evaluation form the device runs)
+//   libm_check theta        -> "bad <count>": theta_of(k) against torch's expression, all 2^24 k
 //   libm_check consts       -> the header's logf / sincosf constants, one %a per line, in the
 //                              order tools/libm_float_consts.py lists glibc's
 #include <math.h>
@@ -61,11 +63,13 @@ int main(int argc, char** argv) {
     printf("bad %ld\n", bad);
     return 0;
   }
+  const bool fused = argc > 2 && !strcmp(argv[2], "fma");
   if (!strcmp(argv[1], "logf")) {
     long bad = 0;
     for (uint32_t k = 0; k < (1u << 24); k++) {
       const float u1 = 1.0f - (float)k * (1.0f / 16777216.0f);
-      if (fks_libm::fbits(fks_libm::logf_glibc(u1)) != fks_libm::fbits(logf(u1))) bad++;
+      const float mine = fused ? fks_libm::logf_glibc<true>(u1) : fks_libm::logf_glibc<false>(u1);
+      if (fks_libm::fbits(mine) != fks_libm::fbits(logf(u1))) bad++;
     }
     printf("bad %ld\n", bad);
     return 0;
@@ -75,9 +79,20 @@ int main(int argc, char** argv) {
     for (uint32_t k = 0; k < (1u << 24); k++) {
       const float th = (float)(2.0f * 3.14159265358979323846 * (double)((float)k * (1.0f / 16777216.0f)));
       float s, c;
-      fks_libm::sincosf_glibc(th, s, c);
+      if (fused) fks_libm::sincosf_glibc<true>(th, s, c);
+      else fks_libm::sincosf_glibc<false>(th, s, c);
       if (fks_libm::fbits(s) != fks_libm::fbits(sinf(th))) bad++;
       if (fks_libm::fbits(c) != fks_libm::fbits(cosf(th))) bad++;
+    }
+    printf("bad %ld\n", bad);
+    return 0;
+  }
+  if (!strcmp(argv[1], "theta")) {
+    long bad = 0;
+    for (uint32_t k = 0; k < (1u << 24); k++) {
+      const float u2 = (float)k * (1.0f / 16777216.0f);
+      const float ref = (float)(2.0f * 3.14159265358979323846 * (double)u2);
+      if (fks_libm::fbits(fks_libm::theta_of(k)) != fks_libm::fbits(ref)) bad++;
     }
     printf("bad %ld\n", bad);
     return 0;

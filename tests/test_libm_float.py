@@ -28,17 +28,23 @@ def checker(tmp_path_factory):
     return exe
 
 
-def _run(exe, mode, tunables=None):
+def _run(exe, mode, tunables=None, *args):
     env = dict(os.environ)
     if tunables:
         env["GLIBC_TUNABLES"] = tunables
-    return subprocess.run([str(exe), mode], capture_output=True, text=True, check=True, env=env).stdout
+    return subprocess.run([str(exe), mode, *args], capture_output=True, text=True, check=True, env=env).stdout
 
 
+@pytest.mark.parametrize("form", ["plain", "fma"])  # glibc's source order / the fused form the device runs
 @pytest.mark.parametrize("tunables", [None, NO_FMA])
 @pytest.mark.parametrize("fn", ["logf", "sincosf"])
-def test_every_input_equals_glibc(checker, fn, tunables):
-    assert _run(checker, fn, tunables).split() == ["bad", "0"]
+def test_every_input_equals_glibc(checker, fn, tunables, form):
+    assert _run(checker, fn, tunables, form).split() == ["bad", "0"]
+
+
+def test_theta_form(checker):
+    """fks_libm::theta_of -- the device's angle -- is torch's expression on every b < 2^24."""
+    assert _run(checker, "theta").split() == ["bad", "0"]
 
 
 def test_tunables_mask_fma():
