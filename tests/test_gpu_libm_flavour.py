@@ -12,9 +12,9 @@ checks them on every input of the path against the host's glibc).
   the oracle's CAP_DEFAULT restatement, with bf16 and short tensors in the same lists
   (whose z the flavour does not change);
 * torch itself: a subprocess under ATEN_CPU_CAPABILITY=default, where the codec picks the
-  flavour from torch's capability, runs the drop-in reconstruct_ on the GPU and the
-  reference's update loop as torch ops on CPU tensors (oracle/torch_replica.py), bit for
-  bit, generator state included.
+  flavour from torch's capability, runs the drop-in reconstruct_ and three zeroth-order
+  steps on the GPU and the reference's loop and steps as torch ops on CPU tensors
+  (oracle/torch_replica.py), bit for bit, generator state included.
 """
 import os
 import subprocess
@@ -163,6 +163,29 @@ for i, (p, r) in enumerate(zip(params, ref)):
     a, b = p.detach().cpu().view(torch.int32), r.view(torch.int32)
     assert torch.equal(a, b), (i, int((a != b).sum()))
 assert torch.equal(got_state, torch.get_rng_state()), "CPU generator"
+
+# zeroth-order steps (perturb +1 / -2 / +1, then the update): the drop-in optimizer on the
+# GPU copy against the reference's step on the CPU copy; the loss is a float64 sum taken on
+# the CPU from the same bits on both sides
+from fate_llm.algo.fedkseed.optimizer import ZerothOrderOptimizer
+params_c = [torch.nn.Parameter(r.clone()) for r in ref]
+def groups(ps):
+    return [{"params": ps[:2], "weight_decay": 0.0, "lr": 1e-4, "eps": 1e-3},
+            {"params": ps[2:], "weight_decay": 0.01, "lr": 1e-4, "eps": 1e-3}]
+def closure_on(ps):
+    return lambda: torch.stack([(p.detach().cpu().double() * (i + 1)).sum() for i, p in enumerate(ps)]).sum()
+opt = ZerothOrderOptimizer(groups(params), lr=1e-4, eps=1e-3, weight_decay=0.01, grad_clip=0.0)
+rg = groups(params_c)
+for step, seed in enumerate([23, 2**35 + 1, 23]):
+    g_ref, lr_ref, ll_ref = R.zeroth_order_step(rg, seed, closure_on(params_c), 1e-3)
+    want = torch.get_rng_state()
+    torch.manual_seed(999)  # the drop-in must move the generator itself
+    g_got, lr_got, ll_got = opt.zeroth_order_step(seed, closure_on(params))
+    assert float(lr_got) == float(lr_ref) and float(ll_got) == float(ll_ref) and float(g_got) == float(g_ref), step
+    for i, (p, r) in enumerate(zip(params, params_c)):
+        a, b = p.detach().cpu().view(torch.int32), r.detach().view(torch.int32)
+        assert torch.equal(a, b), (step, i, int((a != b).sum()))
+    assert torch.equal(torch.get_rng_state(), want), f"step {step}: CPU generator"
 print("ok")
 '''
 

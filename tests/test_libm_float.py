@@ -134,3 +134,30 @@ def test_wire_tag_carries_the_flavour():
     buf[6:8] = flags.to_bytes(2, "little")
     with pytest.raises(P.WireFormatError):
         P.decode_history(bytes(buf))
+
+
+def test_client_declares_the_flavour_for_fp32_models():
+    """ClientTrainer's declared stream (what its histories carry): "torch_cpu_libm" for a
+    model with fp32 tensors of >= 16 elements on the libm flavour, "torch_cpu" otherwise."""
+    import torch
+    from fate_llm.algo.fedkseed import codec
+    from fate_llm.algo.fedkseed import fedkseed as F
+
+    class Args:
+        learning_rate, weight_decay, device = 1e-3, 0.0, torch.device("cpu")
+
+    def client(model):
+        return F.ClientTrainer(None, model, F.FedKSeedTrainingArguments(), Args(), None, None, None, None)
+
+    old = codec.get_stream_mode()
+    codec.set_stream_mode("torch_cpu")
+    try:
+        codec.set_cpu_fp32_flavour("libm")
+        assert client(torch.nn.Linear(8, 8)).stream_mode == "torch_cpu_libm"
+        assert client(torch.nn.Linear(8, 8).to(torch.bfloat16)).stream_mode == "torch_cpu"
+        assert client(torch.nn.Linear(2, 3)).stream_mode == "torch_cpu"  # 6 + 3 elements: the serial path
+        codec.set_cpu_fp32_flavour("avx")
+        assert client(torch.nn.Linear(8, 8)).stream_mode == "torch_cpu"
+    finally:
+        codec.set_cpu_fp32_flavour(None)
+        codec.set_stream_mode(old)
