@@ -43,6 +43,9 @@ constexpr int kBsFence = 8;      // slice kernel: compiler fence after every 8 s
 #ifndef FKS_LOG_INTMASK          // fp32 Cephes log: the x < sqrt(1/2) select as integer arithmetic
 #define FKS_LOG_INTMASK 1
 #endif
+#ifndef FKS_F32_TRIM             // fp32 Cephes z: the uniforms' scalings folded, the sincos signs
+#define FKS_F32_TRIM 1           // as one v_bitop3 each (same values; 0 = the round-5 form, for A/B)
+#endif
 
 namespace fks {
 namespace {
@@ -55,6 +58,7 @@ __device__ __forceinline__ uint32_t mt_twist(uint32_t u, uint32_t v) {
 // v_bitop3_b32 truth tables (LOP3 convention: f(0xF0, 0xCC, 0xAA))
 constexpr unsigned kXorAnd = 0x78;  // a ^ (b & c)
 constexpr unsigned kXorMask = 0x28; // (a ^ b) & c
+constexpr unsigned kXorNotAnd = 0xD2;  // a ^ (~b & c)
 
 // tempering, MT19937RNGEngine.h:141-145; each "y ^= (y << s) & M" is one shift + one bitop3
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
@@ -921,8 +925,18 @@ __device__ __forceinline__ void cephes_sincosf_nonneg(float x, float& s, float& 
   ys = __fmaf_rn(ys, x, x);
   const float xmm1 = poly_mask ? ys : yc;
   const float xmm2 = poly_mask ? yc : ys;
+#if FKS_F32_TRIM
+  // sign_bit_sin = bit 2 of imm2 at bit 31; sign_bit_cos = bit 2 of ~(imm2 - 2), i.e. the
+  // complement of bit 31 of (imm2 << 29) - (2 << 29): one v_bitop3 each
+  (void)sign_bit_sin;
+  (void)sign_bit_cos;
+  const uint32_t sh = (uint32_t)imm2 << 29;
+  s = __uint_as_float(__builtin_amdgcn_bitop3_b32(__float_as_uint(xmm1), sh, 0x80000000u, kXorAnd));
+  c = __uint_as_float(__builtin_amdgcn_bitop3_b32(__float_as_uint(xmm2), sh - 0x40000000u, 0x80000000u, kXorNotAnd));
+#else
   s = __uint_as_float(__float_as_uint(xmm1) ^ sign_bit_sin);
   c = __uint_as_float(__float_as_uint(xmm2) ^ sign_bit_cos);
+#endif
 }
 
 // Correctly rounded sqrt of the radius input x = -2 log(u1), as _mm256_sqrt_ps: the
@@ -976,11 +990,20 @@ __device__ __forceinline__ void z_pair_f32_raw(uint32_t r1, uint32_t r2, float& 
   w.x = r1;
   w.y = r2;
   const u32x2_t t = temper_pair_u24(w);
+#if FKS_F32_TRIM
+  // u1 = 1 - d1 (exact: d1 = t.x 2^-24) as one fma; theta = RN(2pi_f * t.y 2^-24) =
+  // RN((2pi_f 2^-24) * t.y), the power-of-two scaling exact: one multiply
+  const float u1 = __fmaf_rn((float)t.x, -1.0f / 16777216.0f, 1.0f);
+  const float theta = (float)t.y * (6.28318548202514648438f / 16777216.0f);
+#else
   const float d1 = (float)t.x * (1.0f / 16777216.0f);
   const float d2 = (float)t.y * (1.0f / 16777216.0f);
-  const float radius = radius_sqrt(-2.0f * cephes_logf(1.0f - d1));
+  const float u1 = 1.0f - d1;
+  const float theta = 6.28318548202514648438f * d2;
+#endif
+  const float radius = radius_sqrt(-2.0f * cephes_logf(u1));
   float s, c;
-  cephes_sincosf_nonneg(6.28318548202514648438f * d2, s, c);
+  cephes_sincosf_nonneg(theta, s, c);
   z1 = __fmaf_rn(radius, c, 0.0f);
   z2 = __fmaf_rn(radius, s, 0.0f);
 }
