@@ -1025,7 +1025,7 @@ __device__ __forceinline__ void z_pair_f32_libm(uint32_t tab, uint32_t r1, uint3
   w.x = r1;
   w.y = r2;
   const u32x2_t t = temper_pair_u24(w);
-  const float u1 = 1.0f - (float)t.x * (1.0f / 16777216.0f);  // 1 - data[j]
+  const float u1 = __fmaf_rn((float)t.x, -1.0f / 16777216.0f, 1.0f);  // 1 - data[j], exact
   const f64x2_t e = *(const lds_f64x2_t*)(size_t)(tab + 16u * (uint32_t)fks_libm::logf_index(u1));
   const float radius = radius_sqrt(-2.0f * fks_libm::logf_core<true>(u1, e.x, e.y));
   const float theta = fks_libm::theta_of(t.y);  // 2.0f * c10::pi<double> * data[j + 8]
