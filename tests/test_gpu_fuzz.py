@@ -109,6 +109,38 @@ def test_random_call_matches_oracle(case):
             assert hits1 > hits0, f"{what}: the warm call found no seed in the window cache"
 
 
+@pytest.mark.parametrize("case", range(16))
+def test_random_call_libm_flavour_matches_oracle(case):
+    """The same sweep on the CPU stream's libm flavour (ATen's DEFAULT capability: glibc's
+    logf / sinf / cosf for fp32), fp32-heavy layouts, against the oracle's
+    CAP_DEFAULT path; element shards and the window cache as above."""
+    from fate_llm.algo.fedkseed import codec
+    dev = _dev()
+    rng = np.random.default_rng(7000 + case)
+    sizes, dtypes, lrs, wds, seeds, vals, nshards, jwin = _config(rng)
+    dtypes = ["float32" if rng.random() < 0.75 else d for d in dtypes]
+    g = torch.Generator().manual_seed(case)
+    base = [to_np((torch.randn(n, generator=g) * 0.02).to(TD[d])) for n, d in zip(sizes, dtypes)]
+    ks = [s for s, v in zip(seeds, vals) if v != 0.0]
+    kv = [v for v in vals if v != 0.0]
+    ref = [a.copy() for a in base]
+    O.reconstruct(ref, [DTC[d] for d in dtypes], lrs, wds, seeds, vals, O.CAP_DEFAULT)
+    what = f"libm case {case}: sizes {sizes} dtypes {dtypes} wds {wds} k {len(seeds)} shards {nshards} jwin {jwin}"
+    codec.set_cpu_fp32_flavour("libm")
+    try:
+        for label in (("cold", "warm") if jwin else ("cold",)):
+            ts = [from_np(a, d, dev) for a, d in zip(base, dtypes)]
+            specs = [codec.ParamSpec(t, lr=lr, weight_decay=wd) for t, lr, wd in zip(ts, lrs, wds)]
+            if ks:
+                for r in range(nshards):
+                    codec.directional_step(specs, ks, kv, shard=r, nshards=nshards, cache_windows=jwin)
+            torch.cuda.synchronize()
+            for t, r_, d in zip(ts, ref, dtypes):
+                assert_bitwise(to_np(t), r_, d, f"{what} ({label})")
+    finally:
+        codec.set_cpu_fp32_flavour(None)
+
+
 def _rocm_reference(params, seeds, vals, lrs, wds):
     """zo_utils.directional_derivative_step's torch calls on the device (zo_utils.py:42-52),
     per-tensor lr / wd as the codec's ParamSpecs carry them."""

@@ -186,6 +186,18 @@ for step, seed in enumerate([23, 2**35 + 1, 23]):
         a, b = p.detach().cpu().view(torch.int32), r.detach().view(torch.int32)
         assert torch.equal(a, b), (step, i, int((a != b).sum()))
     assert torch.equal(torch.get_rng_state(), want), f"step {step}: CPU generator"
+# the same with the loss handed over as a device tensor (the optimizer's fused device path:
+# perturb +1 / -2 on the GPU, g and the restore + update from device memory)
+for step, seed in enumerate([41, 2**36 + 3]):
+    g_ref, lr_ref, ll_ref = R.zeroth_order_step(rg, seed, closure_on(params_c), 1e-3)
+    want = torch.get_rng_state()
+    torch.manual_seed(998)
+    g_got, lr_got, ll_got = opt.zeroth_order_step(seed, lambda: closure_on(params)().cuda())
+    assert float(lr_got) == float(lr_ref) and float(ll_got) == float(ll_ref) and float(g_got) == float(g_ref), step
+    for i, (p, r) in enumerate(zip(params, params_c)):
+        a, b = p.detach().cpu().view(torch.int32), r.detach().view(torch.int32)
+        assert torch.equal(a, b), ("device loss", step, i, int((a != b).sum()))
+    assert torch.equal(torch.get_rng_state(), want), f"device-loss step {step}: CPU generator"
 print("ok")
 '''
 
