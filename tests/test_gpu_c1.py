@@ -9,7 +9,8 @@ in the dict's insertion order, exact zeros skipped.
 
 Random-init weights of that architecture (no network for the checkpoint); the bench's
 K=4096 (seed, scalar) list (4055 non-zero).  Checked, for weight decay 0.0 (the HF default
-the tutorial leaves in place) and 0.01:
+the tutorial leaves in place) and 0.01, and at 0.0 on the libm flavour (a reference host under
+ATen's DEFAULT CPU capability):
 
   * 8 element shards run one after another == the whole reconstruct, bit for bit;
   * the list applied as two calls (2048 + 2007 non-zero seeds) == one call;
@@ -57,8 +58,19 @@ def model_0():
     return _gpt2_124m()
 
 
-@pytest.mark.parametrize("wd", [0.0, 0.01])
-def test_c1_gpt2_124m_fp32_k4096(model_0, wd):
+@pytest.mark.parametrize("wd,flavour", [(0.0, "avx"), (0.01, "avx"), (0.0, "libm")])
+def test_c1_gpt2_124m_fp32_k4096(model_0, wd, flavour):
+    """flavour "libm": the same run as a reference host under ATen's DEFAULT CPU capability
+    draws it (glibc's logf / sinf / cosf for every fp32 tensor)."""
+    from fate_llm.algo.fedkseed import codec
+    codec.set_cpu_fp32_flavour(flavour)
+    try:
+        _c1(model_0, wd, O.CAP_DEFAULT if flavour == "libm" else O.CAP_AVX2)
+    finally:
+        codec.set_cpu_fp32_flavour(None)
+
+
+def _c1(model_0, wd, cap):
     sys.path.insert(0, ROOT)
     import bench
     from fate_llm.algo.fedkseed import codec
@@ -108,7 +120,7 @@ def test_c1_gpt2_124m_fp32_k4096(model_0, wd):
     wte0 = model_0.transformer.wte.weight.detach().reshape(-1)[:PREFIX].numpy().copy()
     assert groups0[1]["params"][0] is model_0.transformer.wte.weight
     ref = [a.copy() for a in no_decay0] + [wte0.copy()]
-    O.reconstruct(ref, [O.F32] * len(ref), [1e-5] * len(ref), [wd] * len(ref), ks, kv)
+    O.reconstruct(ref, [O.F32] * len(ref), [1e-5] * len(ref), [wd] * len(ref), ks, kv, cap)
     got_nd = [p.detach().reshape(-1).cpu().numpy() for p in g_whole[0]["params"]]
     moved = 0
     for i, (g, r, p0) in enumerate(zip(got_nd, ref, no_decay0)):
