@@ -183,6 +183,8 @@ def main():
         "GBps_extrapolated": round(need / t_full / 1e9, 4),
         "seed_param_per_s": round(total * 19 / per_pass, 1),
         "data": "synthetic: random-init N(0, 0.02^2) fp32, seeds/scalars of bench.synthetic_seeds(4096)",
+        "stream": codec.resolve_stream_mode("cuda"),
+        "fp32_flavour": codec.cpu_fp32_flavour(),
     }
     if verify is not None:
         out["verify"] = verify
