@@ -151,6 +151,11 @@ assert torch.backends.cpu.get_cpu_capability() == "DEFAULT"
 assert codec.cpu_fp32_flavour() == "libm" and codec.get_stream_mode() == "torch_cpu"
 g = torch.Generator().manual_seed(3)
 init = [torch.randn(n, generator=g) * 0.02 for n in (4096, 1000, 7, 65552, 33)]
+init.append((torch.randn(5000, generator=g) * 0.02).to(torch.bfloat16))  # bf16 draws the same z under either capability
+
+
+def bits(t):
+    return t.view(torch.int16 if t.element_size() == 2 else torch.int32)
 seeds = [17, 2**32 + 1, 5, 90210]
 vals = [2.0, -0.5, 0.0, 1.25]
 lr, wd = 1e-3, 0.01
@@ -160,7 +165,7 @@ got_state = torch.get_rng_state()
 ref = [t.clone() for t in init]
 R.reconstruct(ref, seeds, vals, lr, wd)  # the reference's loop: torch.normal on CPU tensors
 for i, (p, r) in enumerate(zip(params, ref)):
-    a, b = p.detach().cpu().view(torch.int32), r.view(torch.int32)
+    a, b = bits(p.detach().cpu()), bits(r)
     assert torch.equal(a, b), (i, int((a != b).sum()))
 assert torch.equal(got_state, torch.get_rng_state()), "CPU generator"
 
@@ -183,7 +188,7 @@ for step, seed in enumerate([23, 2**35 + 1, 23]):
     g_got, lr_got, ll_got = opt.zeroth_order_step(seed, closure_on(params))
     assert float(lr_got) == float(lr_ref) and float(ll_got) == float(ll_ref) and float(g_got) == float(g_ref), step
     for i, (p, r) in enumerate(zip(params, params_c)):
-        a, b = p.detach().cpu().view(torch.int32), r.detach().view(torch.int32)
+        a, b = bits(p.detach().cpu()), bits(r.detach())
         assert torch.equal(a, b), (step, i, int((a != b).sum()))
     assert torch.equal(torch.get_rng_state(), want), f"step {step}: CPU generator"
 # the same with the loss handed over as a device tensor (the optimizer's fused device path:
@@ -195,7 +200,7 @@ for step, seed in enumerate([41, 2**36 + 3]):
     g_got, lr_got, ll_got = opt.zeroth_order_step(seed, lambda: closure_on(params)().cuda())
     assert float(lr_got) == float(lr_ref) and float(ll_got) == float(ll_ref) and float(g_got) == float(g_ref), step
     for i, (p, r) in enumerate(zip(params, params_c)):
-        a, b = p.detach().cpu().view(torch.int32), r.detach().view(torch.int32)
+        a, b = bits(p.detach().cpu()), bits(r.detach())
         assert torch.equal(a, b), ("device loss", step, i, int((a != b).sum()))
     assert torch.equal(torch.get_rng_state(), want), f"device-loss step {step}: CPU generator"
 print("ok")
